@@ -1,0 +1,202 @@
+// C-ABI surface of libflite_hip.so (declared in include/flite.h). Plain pointers and sizes only; every
+// entry point returns an int status (0 = ok) and never throws; the last error message is thread-local.
+#include <string>
+
+#include "../../include/flite.h"
+#include "common.h"
+#include "kernels.h"
+#include "dit.h"
+#include <math.h>
+
+namespace flite {
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+const char* get_last_error() { return g_last_error.c_str(); }
+}  // namespace flite
+
+using namespace flite;
+
+extern "C" {
+
+const char* flite_last_error(void) { return get_last_error(); }
+
+int flite_version(void) { return FLITE_ABI_VERSION; }
+
+int flite_gemm_bf16(void* stream, int M, int N, int K, const void* A, long lda, const void* W, long ldw,
+                    const void* W2, const void* bias, int epilogue, void* out, long ldo, const float* gate,
+                    long gate_seg_stride, int rows_per_seg) {
+  GemmParams p;
+  p.A = (const bf16_t*)A;
+  p.lda = lda;
+  p.W = (const bf16_t*)W;
+  p.ldw = ldw;
+  p.W2 = (const bf16_t*)W2;
+  p.bias = (const bf16_t*)bias;
+  p.out = out;
+  p.ldo = ldo;
+  p.gate = gate;
+  p.gate_seg_stride = gate_seg_stride;
+  p.rows_per_seg = rows_per_seg;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  return gemm_bf16(p, epilogue, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------
+extern "C" {
+
+int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void* v, void* o, long q_row_stride,
+                          long k_row_stride, long v_row_stride, long o_row_stride, long head_stride,
+                          const int* cu_seqlens_q, const int* cu_seqlens_k, int batch, int num_heads, int head_dim,
+                          int max_seqlen_q, float softmax_scale) {
+  AttnParams a;
+  a.q = (const bf16_t*)q;
+  a.k = (const bf16_t*)k;
+  a.v = (const bf16_t*)v;
+  a.o = (bf16_t*)o;
+  a.q_row_stride = q_row_stride;
+  a.k_row_stride = k_row_stride;
+  a.v_row_stride = v_row_stride;
+  a.o_row_stride = o_row_stride;
+  a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = head_stride;
+  a.cu_q = cu_seqlens_q;
+  a.cu_k = cu_seqlens_k;
+  a.B = batch;
+  a.H = num_heads;
+  a.head_dim = head_dim;
+  a.max_q = max_seqlen_q;
+  a.scale = softmax_scale;
+  return attn_fwd(a, (hipStream_t)stream);
+}
+
+int flite_rmsnorm_modulate(void* stream, const void* x, int x_is_bf16, long ldx, void* y, long ldy, const void* w,
+                           const float* shift, const float* scale, long mod_seg_stride, long seg_rows, long rows,
+                           int dim, float eps) {
+  NormModParams p;
+  p.x = x;
+  p.ldx = ldx;
+  p.y = (bf16_t*)y;
+  p.ldy = ldy;
+  p.w = (const bf16_t*)w;
+  p.shift = shift;
+  p.scale = scale;
+  p.mod_seg_stride = mod_seg_stride;
+  p.rows = rows;
+  p.D = dim;
+  p.eps = eps;
+  p.in_seg = seg_rows;
+  p.in_stride = seg_rows;
+  p.in_off = 0;
+  return rmsnorm_mod(p, x_is_bf16 != 0, (hipStream_t)stream);
+}
+
+int flite_rope_qknorm(void* stream, void* x, long ldx, long rows, int heads, int rope_heads, const float* cos_t,
+                      const float* sin_t, long tokens_per_seq, float eps) {
+  RopeNormParams p;
+  p.x = (bf16_t*)x;
+  p.ldx = ldx;
+  p.rows = rows;
+  p.heads = heads;
+  p.rope_heads = rope_heads;
+  p.cos = cos_t;
+  p.sin = sin_t;
+  p.tokens_per_seq = tokens_per_seq;
+  p.eps = eps;
+  return rope_qknorm(p, (hipStream_t)stream);
+}
+
+int flite_rope_tables(void* stream, float* cos_t, float* sin_t, int h, int w, int n_reg, float base,
+                      int round_bf16) {
+  float inv[64];
+  for (int i = 0; i < 64; ++i) inv[i] = (float)(1.0 / pow((double)base, (double)(2 * i) / 128.0));
+  float* dinv = nullptr;
+  FLITE_HIP_CHECK(hipMalloc(&dinv, sizeof(inv)));
+  FLITE_HIP_CHECK(hipMemcpy(dinv, inv, sizeof(inv), hipMemcpyHostToDevice));
+  const int rc = rope_table(dinv, cos_t, sin_t, h, w, n_reg, round_bf16, (hipStream_t)stream);
+  FLITE_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+  hipFree(dinv);
+  return rc;
+}
+
+int flite_timestep_embedding(void* stream, const float* t, void* emb, int n, int dim, int quantize) {
+  return timestep_embed(t, (bf16_t*)emb, n, dim, quantize, (hipStream_t)stream);
+}
+
+struct flite_dit {
+  flite::DitEngine* eng;
+};
+
+int flite_dit_create(const flite_dit_config* cfg, flite_dit** out) {
+  FLITE_REQUIRE(cfg != nullptr && out != nullptr, "flite_dit_create: null argument");
+  FLITE_REQUIRE(cfg->depth > 0 && cfg->hidden_size > 0 && cfg->num_heads > 0, "flite_dit_create: bad config");
+  if (gemm_init()) return 1;
+  if (attn_init()) return 1;
+  flite_dit* d = new flite_dit;
+  d->eng = new DitEngine(*cfg);
+  *out = d;
+  return 0;
+}
+
+int flite_dit_destroy(flite_dit* dit) {
+  if (dit) {
+    delete dit->eng;
+    delete dit;
+  }
+  return 0;
+}
+
+int flite_dit_bind(flite_dit* dit, const char* name, const void* ptr, long numel) {
+  FLITE_REQUIRE(dit && name, "flite_dit_bind: null argument");
+  return dit->eng->bind(name, ptr, numel);
+}
+
+int flite_dit_prepare(flite_dit* dit, int batch, int latent_h, int latent_w, int n_ctx, int n_t) {
+  FLITE_REQUIRE(dit, "flite_dit_prepare: null engine");
+  return dit->eng->prepare(batch, latent_h, latent_w, n_ctx, n_t);
+}
+
+int flite_dit_set_context(flite_dit* dit, void* stream, const void* ctx, const int* cu_seqlens_host, int batch) {
+  FLITE_REQUIRE(dit && cu_seqlens_host, "flite_dit_set_context: null argument");
+  return dit->eng->set_context((hipStream_t)stream, ctx, cu_seqlens_host, batch);
+}
+
+int flite_dit_set_timesteps(flite_dit* dit, void* stream, const float* t, int n, int quantize) {
+  FLITE_REQUIRE(dit && t, "flite_dit_set_timesteps: null argument");
+  return dit->eng->set_timesteps((hipStream_t)stream, t, n, quantize);
+}
+
+int flite_gather_rows(void* stream, const void* src, void* dst, const int* idx, long n, int cols) {
+  return gather_rows((const bf16_t*)src, (bf16_t*)dst, idx, n, cols, (hipStream_t)stream);
+}
+
+int flite_dit_forward(flite_dit* dit, void* stream, const void* x, int x_is_bf16, int batch, int t_row0,
+                      int t_row_step, void* out, int out_is_bf16) {
+  FLITE_REQUIRE(dit && x && out, "flite_dit_forward: null argument");
+  if (dit->eng->forward((hipStream_t)stream, x, x_is_bf16 != 0, batch, 1, t_row0, t_row_step)) return 1;
+  return dit->eng->unpatchify_out((hipStream_t)stream, out, out_is_bf16 != 0);
+}
+
+int flite_dit_sample(flite_dit* dit, void* stream, float* acc, int n_img, int n_steps, const float* t_host,
+                     const float* dt_host, float guidance, int use_cfg, int apg, float apg_threshold,
+                     int use_graph) {
+  FLITE_REQUIRE(dit && acc && t_host && dt_host, "flite_dit_sample: null argument");
+  return dit->eng->sample((hipStream_t)stream, acc, n_img, n_steps, t_host, dt_host, guidance, use_cfg, apg,
+                          apg_threshold, use_graph);
+}
+
+}  // extern "C"
+
+extern "C" {
+int flite_init_param(void* stream, void* out, int out_is_bf16, long numel, const char* name, unsigned long long seed,
+                     double std, int ones) {
+  FLITE_REQUIRE(out && name, "flite_init_param: null argument");
+  if (ones) {
+    FLITE_REQUIRE(out_is_bf16, "flite_init_param: ones only for bf16");
+    return fill_bf16((bf16_t*)out, numel, 1.0f, (hipStream_t)stream);
+  }
+  return hash_init(out, out_is_bf16, numel, name, seed, std, (hipStream_t)stream);
+}
+}  // extern "C"

@@ -1,0 +1,604 @@
+// Native DiT engine (host side). See dit.h.
+#include "dit.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+namespace flite {
+
+namespace {
+constexpr int HEAD_DIM = 256;
+
+bool parse_block(const std::string& name, int* idx, std::string* rest) {
+  if (name.rfind("blocks.", 0) != 0) return false;
+  const size_t dot = name.find('.', 7);
+  if (dot == std::string::npos) return false;
+  *idx = atoi(name.substr(7, dot - 7).c_str());
+  *rest = name.substr(dot + 1);
+  return true;
+}
+}  // namespace
+
+DitEngine::DitEngine(const flite_dit_config& c) : cfg(c) {
+  D = c.hidden_size;
+  H = c.num_heads;
+  F = c.mlp_hidden;
+  R = c.n_register_tokens;
+  P = c.patch_size;
+  C = c.in_channels;
+  w_.blocks.resize(c.depth);
+  for (int i = 0; i < c.depth; ++i)
+    w_.blocks[i].cross = c.per_block_adaln ? true : (i % 4 == 0 || i < 8);  // model.py:464 / model_v2.py:468
+}
+
+DitEngine::~DitEngine() {
+  free_ws();
+  if (gexec_) hipGraphExecDestroy(gexec_);
+  if (gstream_) hipStreamDestroy(gstream_);
+  if (ev_in_) hipEventDestroy(ev_in_);
+  if (ev_out_) hipEventDestroy(ev_out_);
+}
+
+void DitEngine::free_ws() {
+  for (void* p : allocs_) hipFree(p);
+  allocs_.clear();
+  ctx_kv_.clear();
+}
+
+int DitEngine::alloc(void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  FLITE_HIP_CHECK(hipMalloc(p, bytes));
+  allocs_.push_back(*p);
+  return 0;
+}
+
+int DitEngine::bind(const std::string& name, const void* ptr, long numel) {
+  FLITE_REQUIRE(ptr != nullptr, "bind: null pointer for " + name);
+  FLITE_REQUIRE(((uintptr_t)ptr & 15) == 0, "bind: parameter " + name + " is not 16-B aligned");
+  bound_[name] = {ptr, numel};
+  const bf16_t* p = (const bf16_t*)ptr;
+  const long DD = (long)D * D;
+  auto expect = [&](long n) -> int {
+    FLITE_REQUIRE(numel == n, "bind: " + name + " has " + std::to_string(numel) + " elements, expected " +
+                                  std::to_string(n));
+    return 0;
+  };
+  int blk;
+  std::string rest;
+  if (parse_block(name, &blk, &rest)) {
+    FLITE_REQUIRE(blk >= 0 && blk < cfg.depth, "bind: block index out of range in " + name);
+    BlockW& b = w_.blocks[blk];
+    if (rest == "norm1.weight") { if (expect(D)) return 2; b.norm1 = p; }
+    else if (rest == "self_attn.qkv.weight") { if (expect(3 * DD)) return 2; b.qkv_w = p; }
+    else if (rest == "self_attn.qkv.bias") { if (expect(3L * D)) return 2; b.qkv_b = p; }
+    else if (rest == "self_attn.proj.weight") { if (expect(DD)) return 2; b.proj_w = p; }
+    else if (rest == "norm2.weight") { if (expect(D)) return 2; b.norm2 = p; }
+    else if (rest == "cross_attn.q.weight") { if (expect(DD)) return 2; b.cq_w = p; }
+    else if (rest == "cross_attn.q.bias") { if (expect(D)) return 2; b.cq_b = p; }
+    else if (rest == "cross_attn.context_kv.weight") { if (expect(2 * DD)) return 2; b.ckv_w = p; }
+    else if (rest == "cross_attn.context_kv.bias") { if (expect(2L * D)) return 2; b.ckv_b = p; }
+    else if (rest == "cross_attn.proj.weight") { if (expect(DD)) return 2; b.cproj_w = p; }
+    else if (rest == "norm3.weight") { if (expect(D)) return 2; b.norm3 = p; }
+    else if (rest == "mlp.gate_proj.weight") { if (expect((long)F * D)) return 2; b.gate_w = p; }
+    else if (rest == "mlp.up_proj.weight") { if (expect((long)F * D)) return 2; b.up_w = p; }
+    else if (rest == "mlp.down_proj.weight") { if (expect((long)F * D)) return 2; b.down_w = p; }
+    else if (rest == "adaLN_modulation.1.weight") { if (expect(9 * DD)) return 2; b.ada_w = p; }
+    else if (rest == "adaLN_modulation.1.bias") { if (expect(9L * D)) return 2; b.ada_b = p; }
+    else FLITE_REQUIRE(false, "bind: unknown block parameter " + name);
+    return 0;
+  }
+  const long CC = cfg.cross_attn_input_size;
+  const long cpp = (long)C * P * P;
+  if (name == "context_proj.weight") { if (expect(CC * D)) return 2; w_.ctx_proj_w = p; }
+  else if (name == "context_proj.bias") { if (expect(D)) return 2; w_.ctx_proj_b = p; }
+  else if (name == "context_norm.weight") { if (expect(D)) return 2; w_.ctx_norm = p; }
+  else if (name == "patch_embed.patch_proj.weight") { if (expect(cpp * D)) return 2; w_.patch_w = p; }
+  else if (name == "patch_embed.patch_proj.bias") { if (expect(D)) return 2; w_.patch_b = p; }
+  else if (name == "register_tokens") { if (expect((long)R * D)) return 2; w_.registers = p; }
+  else if (name == "time_embed.0.weight") { if (expect(4 * DD)) return 2; w_.te0_w = p; }
+  else if (name == "time_embed.0.bias") { if (expect(4L * D)) return 2; w_.te0_b = p; }
+  else if (name == "time_embed.2.weight") { if (expect(4 * DD)) return 2; w_.te2_w = p; }
+  else if (name == "time_embed.2.bias") { if (expect(D)) return 2; w_.te2_b = p; }
+  else if (name == "adaLN_modulation.1.weight") { if (expect(9 * DD)) return 2; w_.ada_w = p; }
+  else if (name == "adaLN_modulation.1.bias") { if (expect(9L * D)) return 2; w_.ada_b = p; }
+  else if (name == "final_modulation.1.weight") { if (expect(2 * DD)) return 2; w_.fmod_w = p; }
+  else if (name == "final_modulation.1.bias") { if (expect(2L * D)) return 2; w_.fmod_b = p; }
+  else if (name == "final_norm.weight") { if (expect(D)) return 2; w_.fnorm = p; }
+  else if (name == "final_proj.weight") { if (expect(cpp * D)) return 2; w_.fproj_w = p; }
+  else if (name == "final_proj.bias") { if (expect(cpp)) return 2; w_.fproj_b = p; }
+  else FLITE_REQUIRE(false, "bind: unknown parameter " + name);
+  return 0;
+}
+
+int DitEngine::check_bound() {
+  const bool bias = cfg.train_bias_and_rms != 0;
+  FLITE_REQUIRE(w_.ctx_proj_w && w_.ctx_proj_b && w_.ctx_norm, "unbound: context_proj/context_norm");
+  FLITE_REQUIRE(w_.patch_w && w_.patch_b && w_.registers, "unbound: patch_embed/register_tokens");
+  FLITE_REQUIRE(w_.te0_w && w_.te0_b && w_.te2_w && w_.te2_b, "unbound: time_embed");
+  FLITE_REQUIRE(w_.fmod_w && w_.fmod_b && w_.fproj_w && w_.fproj_b, "unbound: final stage");
+  FLITE_REQUIRE(!bias || w_.fnorm, "unbound: final_norm.weight");
+  if (!cfg.per_block_adaln) FLITE_REQUIRE(w_.ada_w && w_.ada_b, "unbound: adaLN_modulation");
+  for (int i = 0; i < cfg.depth; ++i) {
+    const BlockW& b = w_.blocks[i];
+    const std::string pre = "unbound: blocks." + std::to_string(i) + ".";
+    FLITE_REQUIRE(b.norm1 && b.qkv_w && b.proj_w && b.norm3 && b.gate_w && b.up_w && b.down_w, pre + "*");
+    FLITE_REQUIRE(!bias || b.qkv_b, pre + "self_attn.qkv.bias");
+    if (b.cross) {
+      FLITE_REQUIRE(b.norm2 && b.cq_w && b.ckv_w && b.cproj_w, pre + "cross_attn.*");
+      FLITE_REQUIRE(!bias || (b.cq_b && b.ckv_b), pre + "cross_attn biases");
+    }
+    if (cfg.per_block_adaln) FLITE_REQUIRE(b.ada_w && b.ada_b, pre + "adaLN_modulation");
+  }
+  return 0;
+}
+
+int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
+  FLITE_REQUIRE(D % 256 == 0 && D / H == HEAD_DIM, "config: hidden_size / num_heads must be 256");
+  FLITE_REQUIRE(F % 256 == 0 || F % 16 == 0, "config: mlp hidden must be a multiple of 16");
+  FLITE_REQUIRE(Hl % P == 0 && Wl % P == 0, "prepare: latent H, W must be multiples of patch_size");
+  FLITE_REQUIRE(Hl / P <= 512 && Wl / P <= 512, "prepare: RoPE tables cover at most 512x512 patches");
+  FLITE_REQUIRE(cfg.cross_attn_input_size % 64 == 0, "config: cross_attn_input_size must be a multiple of 64");
+  if (check_bound()) return 2;
+  if (B == B_ && Hl == Hl_ && Wl == Wl_ && n_ctx_max <= nctx_max_ && n_t_max <= ntmax_) return 0;
+  free_ws();
+  if (gexec_) {
+    hipGraphExecDestroy(gexec_);
+    gexec_ = nullptr;
+  }
+  B_ = B;
+  Hl_ = Hl;
+  Wl_ = Wl;
+  HW_ = (Hl / P) * (Wl / P);
+  T_ = R + HW_;
+  M_ = (long)B * T_;
+  nctx_max_ = n_ctx_max;
+  ntmax_ = n_t_max;
+  const int cpp = C * P * P;
+  if (alloc((void**)&x_, M_ * D * 4)) return 1;
+  if (alloc((void**)&nbuf_, M_ * D * 2)) return 1;
+  if (alloc((void**)&qkv_, M_ * 3 * D * 2)) return 1;
+  if (alloc((void**)&obuf_, M_ * D * 2)) return 1;
+  if (alloc((void**)&hbuf_, M_ * (long)F * 2)) return 1;
+  if (alloc((void**)&patches_, (long)B * HW_ * cpp * 2)) return 1;
+  if (alloc((void**)&fout_, (long)B * HW_ * cpp * 4)) return 1;
+  if (alloc((void**)&cu_self_, (B + 1) * 4)) return 1;
+  if (alloc((void**)&cu_ctx_, (B + 1) * 4)) return 1;
+  if (alloc((void**)&cos_, (long)T_ * 128 * 4)) return 1;
+  if (alloc((void**)&sin_, (long)T_ * 128 * 4)) return 1;
+  if (alloc((void**)&inv_freq_, 64 * 4)) return 1;
+  if (alloc((void**)&ctx_p_, (long)std::max(n_ctx_max, 1) * D * 2)) return 1;
+  ctx_kv_.assign(cfg.depth, nullptr);
+  for (int i = 0; i < cfg.depth; ++i)
+    if (w_.blocks[i].cross)
+      if (alloc((void**)&ctx_kv_[i], (long)std::max(n_ctx_max, 1) * 2 * D * 2)) return 1;
+  if (alloc((void**)&tdev_, std::max(n_t_max, 1) * 4)) return 1;
+  if (alloc((void**)&temb_, (long)std::max(n_t_max, 1) * D * 2)) return 1;
+  if (alloc((void**)&th_, (long)std::max(n_t_max, 1) * 4 * D * 2)) return 1;
+  if (alloc((void**)&tsilu_, (long)std::max(n_t_max, 1) * D * 2)) return 1;
+  mod_t_stride_ = (long)(cfg.per_block_adaln ? cfg.depth : 1) * 9 * D;
+  if (alloc((void**)&mod_, std::max(n_t_max, 1) * mod_t_stride_ * 4)) return 1;
+  if (alloc((void**)&fmod_, (long)std::max(n_t_max, 1) * 2 * D * 4)) return 1;
+
+  // self-attention cu_seqlens [0, T, 2T, ...] (prepare_flash_attention_inputs with no mask, model.py:549)
+  std::vector<int> cu(B + 1);
+  for (int i = 0; i <= B; ++i) cu[i] = i * T_;
+  FLITE_HIP_CHECK(hipMemcpy(cu_self_, cu.data(), (B + 1) * 4, hipMemcpyHostToDevice));
+  // RoPE inv_freq in double like the reference's python list (model.py:342), then fp32
+  const int rdim = D / (2 * H);  // 128
+  FLITE_REQUIRE(rdim == 128, "config: RoPE dim must be 128");
+  float inv[64];
+  for (int i = 0; i < 64; ++i) inv[i] = (float)(1.0 / pow((double)cfg.rope_base, (double)(2 * i) / (double)rdim));
+  FLITE_HIP_CHECK(hipMemcpy(inv_freq_, inv, sizeof(inv), hipMemcpyHostToDevice));
+  if (rope_table(inv_freq_, cos_, sin_, Hl / P, Wl / P, R, cfg.bf16_rope_tables, 0)) return 1;
+  FLITE_HIP_CHECK(hipDeviceSynchronize());
+  nctx_ = 0;
+  nt_ = 0;
+  return 0;
+}
+
+int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, int nseq) {
+  FLITE_REQUIRE(x_ != nullptr, "set_context: call prepare first");
+  FLITE_REQUIRE(nseq == B_, "set_context: number of context sequences must equal the batch");
+  const int n = cu_host[nseq];
+  FLITE_REQUIRE(n <= nctx_max_, "set_context: context longer than prepared");
+  for (int i = 0; i < nseq; ++i) FLITE_REQUIRE(cu_host[i + 1] >= cu_host[i], "set_context: bad cu_seqlens");
+  FLITE_HIP_CHECK(hipMemcpyAsync(cu_ctx_, cu_host, (nseq + 1) * 4, hipMemcpyHostToDevice, s));
+  nctx_ = n;
+  nseq_ctx_ = nseq;
+  if (n == 0) return 0;
+  // context_proj (model.py:527) -> LigerRMSNorm (model.py:528)
+  GemmParams g;
+  g.A = (const bf16_t*)ctx;
+  g.lda = cfg.cross_attn_input_size;
+  g.W = w_.ctx_proj_w;
+  g.ldw = cfg.cross_attn_input_size;
+  g.bias = w_.ctx_proj_b;
+  g.out = ctx_p_;
+  g.ldo = D;
+  g.M = n;
+  g.N = D;
+  g.K = cfg.cross_attn_input_size;
+  if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+  NormModParams nm;
+  nm.x = ctx_p_;
+  nm.ldx = D;
+  nm.y = ctx_p_;
+  nm.ldy = D;
+  nm.w = w_.ctx_norm;
+  nm.rows = n;
+  nm.D = D;
+  if (rmsnorm_mod(nm, true, s)) return 1;
+  // step-invariant cross-attention K/V (model.py:189-197): context_kv then key QK-norm, cached per block
+  for (int i = 0; i < cfg.depth; ++i) {
+    const BlockW& b = w_.blocks[i];
+    if (!b.cross) continue;
+    GemmParams k;
+    k.A = ctx_p_;
+    k.lda = D;
+    k.W = b.ckv_w;
+    k.ldw = D;
+    k.bias = b.ckv_b;
+    k.out = ctx_kv_[i];
+    k.ldo = 2L * D;
+    k.M = n;
+    k.N = 2 * D;
+    k.K = D;
+    if (gemm_bf16(k, EPI_STORE_BF16, s)) return 1;
+    RopeNormParams rn;
+    rn.x = ctx_kv_[i];
+    rn.ldx = 2L * D;
+    rn.rows = n;
+    rn.heads = H;
+    rn.rope_heads = 0;
+    if (rope_qknorm(rn, s)) return 1;
+  }
+  return 0;
+}
+
+int DitEngine::set_timesteps(hipStream_t s, const float* t_dev, int n, int quantize) {
+  FLITE_REQUIRE(x_ != nullptr, "set_timesteps: call prepare first");
+  FLITE_REQUIRE(n >= 1 && n <= ntmax_, "set_timesteps: too many timesteps for the prepared workspace");
+  if (t_dev != tdev_) FLITE_HIP_CHECK(hipMemcpyAsync(tdev_, t_dev, n * 4, hipMemcpyDeviceToDevice, s));
+  nt_ = n;
+  // timestep_embedding (model.py:20-28,551) -> time_embed Linear-SiLU-Linear (model.py:448-452)
+  if (timestep_embed(tdev_, temb_, n, D, quantize, s)) return 1;
+  GemmParams g;
+  g.A = temb_;
+  g.lda = D;
+  g.W = w_.te0_w;
+  g.ldw = D;
+  g.bias = w_.te0_b;
+  g.out = th_;
+  g.ldo = 4L * D;
+  g.M = n;
+  g.N = 4 * D;
+  g.K = D;
+  g.act = 1;
+  if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+  GemmParams g2;
+  g2.A = th_;
+  g2.lda = 4L * D;
+  g2.W = w_.te2_w;
+  g2.ldw = 4L * D;
+  g2.bias = w_.te2_b;
+  g2.out = tsilu_;  // t_emb only feeds SiLU->Linear heads (adaLN_modulation, final_modulation)
+  g2.ldo = D;
+  g2.M = n;
+  g2.N = D;
+  g2.K = 4 * D;
+  g2.act = 1;
+  if (gemm_bf16(g2, EPI_STORE_BF16, s)) return 1;
+  // adaLN modulation rows (model.py:553-556; model_v2.py:275 per block), fp32
+  auto ada = [&](const bf16_t* W, const bf16_t* b, float* out, long ldo) -> int {
+    GemmParams a;
+    a.A = tsilu_;
+    a.lda = D;
+    a.W = W;
+    a.ldw = D;
+    a.bias = b;
+    a.out = out;
+    a.ldo = ldo;
+    a.M = n;
+    a.N = 9 * D;
+    a.K = D;
+    return gemm_bf16(a, EPI_STORE_F32, s);
+  };
+  if (cfg.per_block_adaln) {
+    for (int i = 0; i < cfg.depth; ++i)
+      if (ada(w_.blocks[i].ada_w, w_.blocks[i].ada_b, mod_ + (long)i * 9 * D, mod_t_stride_)) return 1;
+  } else {
+    if (ada(w_.ada_w, w_.ada_b, mod_, mod_t_stride_)) return 1;
+  }
+  // final modulation (model.py:578): chunk order (shift, scale)
+  GemmParams f;
+  f.A = tsilu_;
+  f.lda = D;
+  f.W = w_.fmod_w;
+  f.ldw = D;
+  f.bias = w_.fmod_b;
+  f.out = fmod_;
+  f.ldo = 2L * D;
+  f.M = n;
+  f.N = 2 * D;
+  f.K = D;
+  if (gemm_bf16(f, EPI_STORE_F32, s)) return 1;
+  return 0;
+}
+
+// One DiTBlock (model.py:270-303). mod points at this block's 9 modulation chunks for segment 0;
+// segment b (= sample b of the CFG batch) reads mod + b * mseg.
+int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
+  const BlockW& b = w_.blocks[blk];
+  const float *shift_sa = mod, *scale_sa = mod + D, *gate_sa = mod + 2L * D;
+  const float *shift_ca = mod + 3L * D, *scale_ca = mod + 4L * D, *gate_ca = mod + 5L * D;
+  const float *shift_mlp = mod + 6L * D, *scale_mlp = mod + 7L * D, *gate_mlp = mod + 8L * D;
+
+  auto norm = [&](const bf16_t* w, const float* sh, const float* sc) -> int {
+    NormModParams nm;
+    nm.x = x_;
+    nm.ldx = D;
+    nm.y = nbuf_;
+    nm.ldy = D;
+    nm.w = w;
+    nm.shift = sh;
+    nm.scale = sc;
+    nm.mod_seg_stride = mseg;
+    nm.rows = M_;
+    nm.D = D;
+    nm.in_seg = T_;
+    nm.in_stride = T_;
+    nm.in_off = 0;
+    return rmsnorm_mod(nm, false, s);
+  };
+  auto resid = [&](const bf16_t* A, long lda, const bf16_t* W, int K, const float* gate) -> int {
+    GemmParams g;
+    g.A = A;
+    g.lda = lda;
+    g.W = W;
+    g.ldw = K;
+    g.out = x_;
+    g.ldo = D;
+    g.gate = gate;
+    g.gate_seg_stride = mseg;
+    g.rows_per_seg = T_;
+    g.M = (int)M_;
+    g.N = D;
+    g.K = K;
+    return gemm_bf16(g, EPI_RESID_F32, s);
+  };
+
+  // --- self attention ---
+  if (norm(b.norm1, shift_sa, scale_sa)) return 1;
+  {
+    GemmParams g;
+    g.A = nbuf_;
+    g.lda = D;
+    g.W = b.qkv_w;
+    g.ldw = D;
+    g.bias = b.qkv_b;
+    g.out = qkv_;
+    g.ldo = 3L * D;
+    g.M = (int)M_;
+    g.N = 3 * D;
+    g.K = D;
+    if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+  }
+  {
+    RopeNormParams rn;
+    rn.x = qkv_;
+    rn.ldx = 3L * D;
+    rn.rows = M_;
+    rn.heads = 2 * H;  // q heads then k heads ("(k h d)" layout, model.py:163)
+    rn.rope_heads = 2 * H;
+    rn.cos = cos_;
+    rn.sin = sin_;
+    rn.tokens_per_seq = T_;
+    if (rope_qknorm(rn, s)) return 1;
+  }
+  {
+    AttnParams a;
+    a.q = qkv_;
+    a.k = qkv_ + D;
+    a.v = qkv_ + 2L * D;
+    a.o = obuf_;
+    a.q_row_stride = a.k_row_stride = a.v_row_stride = 3L * D;
+    a.o_row_stride = D;
+    a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = HEAD_DIM;
+    a.cu_q = cu_self_;
+    a.cu_k = cu_self_;
+    a.B = B_;
+    a.H = H;
+    a.head_dim = HEAD_DIM;
+    a.max_q = T_;
+    a.scale = 1.0f / sqrtf((float)HEAD_DIM);
+    if (attn_fwd(a, s)) return 1;
+  }
+  if (resid(obuf_, D, b.proj_w, D, gate_sa)) return 1;
+
+  // --- cross attention (model.py:291-297) ---
+  if (b.cross) {
+    if (norm(b.norm2, shift_ca, scale_ca)) return 1;
+    GemmParams g;
+    g.A = nbuf_;
+    g.lda = D;
+    g.W = b.cq_w;
+    g.ldw = D;
+    g.bias = b.cq_b;
+    g.out = qkv_;
+    g.ldo = D;
+    g.M = (int)M_;
+    g.N = D;
+    g.K = D;
+    if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+    RopeNormParams rn;
+    rn.x = qkv_;
+    rn.ldx = D;
+    rn.rows = M_;
+    rn.heads = H;
+    rn.rope_heads = 0;
+    if (rope_qknorm(rn, s)) return 1;
+    AttnParams a;
+    a.q = qkv_;
+    a.k = ctx_kv_[blk];
+    a.v = ctx_kv_[blk] + D;
+    a.o = obuf_;
+    a.q_row_stride = D;
+    a.k_row_stride = a.v_row_stride = 2L * D;
+    a.o_row_stride = D;
+    a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = HEAD_DIM;
+    a.cu_q = cu_self_;
+    a.cu_k = cu_ctx_;
+    a.B = B_;
+    a.H = H;
+    a.head_dim = HEAD_DIM;
+    a.max_q = T_;
+    a.scale = 1.0f / sqrtf((float)HEAD_DIM);
+    if (attn_fwd(a, s)) return 1;
+    if (resid(obuf_, D, b.cproj_w, D, gate_ca)) return 1;
+  }
+
+  // --- SwiGLU MLP (model.py:299-301) ---
+  if (norm(b.norm3, shift_mlp, scale_mlp)) return 1;
+  {
+    GemmParams g;
+    g.A = nbuf_;
+    g.lda = D;
+    g.W = b.gate_w;
+    g.W2 = b.up_w;
+    g.ldw = D;
+    g.out = hbuf_;
+    g.ldo = F;
+    g.M = (int)M_;
+    g.N = 2 * F;
+    g.K = D;
+    if (gemm_bf16(g, EPI_SWIGLU_BF16, s)) return 1;
+  }
+  if (resid(hbuf_, F, b.down_w, F, gate_mlp)) return 1;
+  return 0;
+}
+
+int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, int dup, int t_row0, int t_row_step) {
+  FLITE_REQUIRE(x_ != nullptr, "forward: call prepare first");
+  FLITE_REQUIRE(Bi * dup == B_, "forward: batch does not match the prepared workspace");
+  FLITE_REQUIRE(nseq_ctx_ == B_, "forward: set_context must be called for this batch");
+  FLITE_REQUIRE(t_row0 >= 0 && t_row0 + (B_ - 1) * t_row_step < nt_, "forward: timestep rows out of range");
+  const int cpp = C * P * P;
+  // patch embed (model.py:533) straight into the residual stream after the registers (model.py:535)
+  if (patchify(lat, lat_bf16, patches_, Bi, C, Hl_, Wl_, P, dup, s)) return 1;
+  {
+    GemmParams g;
+    g.A = patches_;
+    g.lda = cpp;
+    g.W = w_.patch_w;
+    g.ldw = cpp;
+    g.bias = w_.patch_b;
+    g.out = x_;
+    g.ldo = D;
+    g.M = B_ * HW_;
+    g.N = D;
+    g.K = cpp;
+    g.out_seg = HW_;
+    g.out_seg_stride = T_;
+    g.out_seg_off = R;
+    if (gemm_bf16(g, EPI_STORE_F32, s)) return 1;
+  }
+  if (fill_registers(x_, w_.registers, B_, T_, R, D, s)) return 1;
+  const long mseg = (long)t_row_step * mod_t_stride_;
+  for (int i = 0; i < cfg.depth; ++i) {
+    const float* mod = mod_ + (long)t_row0 * mod_t_stride_ + (cfg.per_block_adaln ? (long)i * 9 * D : 0);
+    if (run_block(s, i, mod, mseg)) return 1;
+  }
+  // final stage (model.py:575-581): drop registers, RMSNorm (fp32 weight multiply), modulate, project
+  {
+    NormModParams nm;
+    nm.x = x_;
+    nm.ldx = D;
+    nm.y = nbuf_;
+    nm.ldy = D;
+    nm.w = cfg.train_bias_and_rms ? w_.fnorm : nullptr;
+    nm.shift = fmod_ + (long)t_row0 * 2 * D;
+    nm.scale = fmod_ + (long)t_row0 * 2 * D + D;
+    nm.mod_seg_stride = (long)t_row_step * 2 * D;
+    nm.rows = (long)B_ * HW_;
+    nm.D = D;
+    nm.in_seg = HW_;
+    nm.in_stride = T_;
+    nm.in_off = R;
+    if (rmsnorm_mod(nm, false, s)) return 1;
+    GemmParams g;
+    g.A = nbuf_;
+    g.lda = D;
+    g.W = w_.fproj_w;
+    g.ldw = D;
+    g.bias = w_.fproj_b;
+    g.out = fout_;
+    g.ldo = cpp;
+    g.M = B_ * HW_;
+    g.N = cpp;
+    g.K = D;
+    if (gemm_bf16(g, EPI_STORE_F32, s)) return 1;
+  }
+  return 0;
+}
+
+int DitEngine::unpatchify_out(hipStream_t s, void* y, bool out_bf16) {
+  return unpatchify(fout_, y, out_bf16, B_, C, Hl_, Wl_, P, s);
+}
+
+int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const float* t_host, const float* dt_host,
+                      float guidance, int use_cfg, int apg, float apg_thr, int use_graph) {
+  FLITE_REQUIRE(n_steps >= 1 && n_steps <= ntmax_, "sample: too many steps for the prepared workspace");
+  const int dup = use_cfg ? 2 : 1;
+  FLITE_REQUIRE(Bi * dup == B_, "sample: batch does not match the prepared workspace");
+  FLITE_REQUIRE(!apg || use_cfg, "sample: APG requires classifier-free guidance");
+  // timesteps: one row per step, shared by every sample of the batch (pipeline.py:260,268)
+  FLITE_HIP_CHECK(hipMemcpyAsync(tdev_, t_host, n_steps * 4, hipMemcpyHostToDevice, s));
+  if (set_timesteps(s, tdev_, n_steps, cfg.bf16_timestep_quant)) return 1;
+
+  auto body = [&](hipStream_t st) -> int {
+    for (int i = 0; i < n_steps; ++i) {
+      if (forward(st, acc, false, Bi, dup, i, 0)) return 1;
+      if (apg) {
+        if (apg_euler(fout_, acc, Bi, C, Hl_, Wl_, P, guidance, apg_thr, dt_host[i], st)) return 1;
+      } else {
+        if (cfg_euler(fout_, acc, Bi, C, Hl_, Wl_, P, dup, guidance, dt_host[i], st)) return 1;
+      }
+    }
+    return 0;
+  };
+  if (!use_graph) return body(s);
+
+  // hipGraph: capture the whole n_steps loop once per (shape, schedule, guidance, accumulator), replay after
+  std::vector<float> key = {(float)n_steps, guidance, (float)use_cfg, (float)apg, apg_thr};
+  for (int i = 0; i < n_steps; ++i) key.push_back(dt_host[i]);
+  if (!gstream_) {
+    FLITE_HIP_CHECK(hipStreamCreateWithFlags(&gstream_, hipStreamNonBlocking));
+    FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
+    FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+  }
+  FLITE_HIP_CHECK(hipEventRecord(ev_in_, s));
+  FLITE_HIP_CHECK(hipStreamWaitEvent(gstream_, ev_in_, 0));
+  if (!gexec_ || key != gkey_ || glat_ != acc) {
+    if (gexec_) {
+      hipGraphExecDestroy(gexec_);
+      gexec_ = nullptr;
+    }
+    hipGraph_t graph;
+    FLITE_HIP_CHECK(hipStreamBeginCapture(gstream_, hipStreamCaptureModeThreadLocal));
+    const int rc = body(gstream_);
+    const hipError_t e = hipStreamEndCapture(gstream_, &graph);
+    if (rc) return rc;
+    FLITE_HIP_CHECK(e);
+    FLITE_HIP_CHECK(hipGraphInstantiate(&gexec_, graph, nullptr, nullptr, 0));
+    hipGraphDestroy(graph);
+    gkey_ = key;
+    glat_ = acc;
+  }
+  FLITE_HIP_CHECK(hipGraphLaunch(gexec_, gstream_));
+  FLITE_HIP_CHECK(hipEventRecord(ev_out_, gstream_));
+  FLITE_HIP_CHECK(hipStreamWaitEvent(s, ev_out_, 0));
+  return 0;
+}
+
+}  // namespace flite

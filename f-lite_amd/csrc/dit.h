@@ -1,0 +1,88 @@
+// Native DiT engine: owns the workspace and drives the per-step forward of f_lite/model.py
+// (DiT.forward, model.py:525-591 / model_v2.py:528-594) and the denoise loop of FLitePipeline.__call__
+// (pipeline.py:250-297) as a sequence of gfx950 kernel launches, optionally captured into one hipGraph.
+#pragma once
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/flite.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace flite {
+
+struct BlockW {
+  bool cross = false;
+  const bf16_t *norm1 = nullptr, *qkv_w = nullptr, *qkv_b = nullptr, *proj_w = nullptr;
+  const bf16_t *norm2 = nullptr, *cq_w = nullptr, *cq_b = nullptr, *ckv_w = nullptr, *ckv_b = nullptr,
+               *cproj_w = nullptr;
+  const bf16_t *norm3 = nullptr, *gate_w = nullptr, *up_w = nullptr, *down_w = nullptr;
+  const bf16_t *ada_w = nullptr, *ada_b = nullptr;  // per-block adaLN (model_v2 layout)
+};
+
+struct DitW {
+  const bf16_t *ctx_proj_w = nullptr, *ctx_proj_b = nullptr, *ctx_norm = nullptr;
+  const bf16_t *patch_w = nullptr, *patch_b = nullptr, *registers = nullptr;
+  const bf16_t *te0_w = nullptr, *te0_b = nullptr, *te2_w = nullptr, *te2_b = nullptr;
+  const bf16_t *ada_w = nullptr, *ada_b = nullptr;  // shared adaLN (model.py layout)
+  const bf16_t *fmod_w = nullptr, *fmod_b = nullptr, *fnorm = nullptr, *fproj_w = nullptr, *fproj_b = nullptr;
+  std::vector<BlockW> blocks;
+};
+
+class DitEngine {
+ public:
+  explicit DitEngine(const flite_dit_config& cfg);
+  ~DitEngine();
+
+  int bind(const std::string& name, const void* ptr, long numel);
+  int check_bound();
+  int prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max);
+  int set_context(hipStream_t s, const void* ctx, const int* cu_host, int nseq);
+  int set_timesteps(hipStream_t s, const float* t_dev, int n, int quantize);
+  // forward of the B = dup*Bi batch; segment b uses timestep row t_row0 + b*t_row_step
+  int forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, int dup, int t_row0, int t_row_step);
+  int unpatchify_out(hipStream_t s, void* y, bool out_bf16);
+  int sample(hipStream_t s, float* acc, int Bi, int n_steps, const float* t_host, const float* dt_host,
+             float guidance, int use_cfg, int apg, float apg_thr, int use_graph);
+
+  const flite_dit_config cfg;
+  int D, H, F, R, P, C;
+
+ private:
+  int run_block(hipStream_t s, int blk, const float* mod, long mseg);
+  int alloc(void** p, size_t bytes);
+  void free_ws();
+
+  DitW w_;
+  std::map<std::string, std::pair<const void*, long>> bound_;
+  std::vector<void*> allocs_;
+  // shape
+  int B_ = 0, Hl_ = 0, Wl_ = 0, T_ = 0, HW_ = 0, ntmax_ = 0, nctx_max_ = 0;
+  long M_ = 0;
+  int nctx_ = 0, nseq_ctx_ = 0;
+  // workspace
+  float* x_ = nullptr;
+  bf16_t *nbuf_ = nullptr, *qkv_ = nullptr, *obuf_ = nullptr, *hbuf_ = nullptr, *patches_ = nullptr;
+  float* fout_ = nullptr;
+  int *cu_self_ = nullptr, *cu_ctx_ = nullptr;
+  float *cos_ = nullptr, *sin_ = nullptr, *inv_freq_ = nullptr;
+  bf16_t* ctx_p_ = nullptr;
+  std::vector<bf16_t*> ctx_kv_;  // per block (cross blocks only)
+  float* tdev_ = nullptr;
+  bf16_t *temb_ = nullptr, *th_ = nullptr;  // sinusoid / hidden
+  bf16_t* tsilu_ = nullptr;                 // silu(t_emb)
+  float* mod_ = nullptr;                    // [n_t][depth or 1][9D]
+  float* fmod_ = nullptr;                   // [n_t][2D]
+  float* apg_scratch_ = nullptr;
+  long mod_t_stride_ = 0;
+  int nt_ = 0;
+  // graph cache
+  hipStream_t gstream_ = nullptr;
+  hipGraphExec_t gexec_ = nullptr;
+  std::vector<float> gkey_;
+  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  const void* glat_ = nullptr;
+};
+
+}  // namespace flite

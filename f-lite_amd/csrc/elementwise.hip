@@ -1,0 +1,469 @@
+// HBM-bound kernels of the DiT step (gfx950). Every kernel reads/writes each element once, vectorised
+// 16 B per lane; reductions are one wave per row with __shfl_xor.
+#include <math.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace flite {
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// RMSNorm (+ weight) (+ adaLN modulate) -> bf16.
+//   y = rmsnorm(x) * w * (1 + scale[seg]) + shift[seg]
+// Reference: LigerRMSNorm (model.py:238,248,260,437) / own RMSNorm (model.py:92-108, final_norm),
+// then `norm_x * (1 + scale) + shift` (model.py:284,293,300,580). Computed in fp32, one rounding.
+// One wave per output row; the input row of output row m is (m / in_seg) * in_stride + in_off + m % in_seg.
+// ------------------------------------------------------------------------------------------------
+template <bool IN_BF16, int NCH>
+__global__ __launch_bounds__(256) void rmsnorm_mod_kernel(NormModParams p) {
+  const int lane = threadIdx.x & 63;
+  const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= p.rows) return;
+  const long seg = p.in_seg > 0 ? m / p.in_seg : 0;
+  const long in_row = p.in_seg > 0 ? seg * p.in_stride + p.in_off + (m % p.in_seg) : m;
+  const int D = p.D;
+  // D == 256 * NCH: lane handles 4 consecutive elements of every 256-wide chunk (registers, static index)
+  float v[4 * NCH];
+  constexpr int nch = NCH;
+  float ss = 0.f;
+  if constexpr (IN_BF16) {
+    const bf16_t* xr = (const bf16_t*)p.x + in_row * p.ldx;
+#pragma unroll
+    for (int c = 0; c < nch; ++c) {
+      const u32x2 w = *(const u32x2*)(xr + c * 256 + lane * 4);
+      v[4 * c + 0] = __uint_as_float(w.x << 16);
+      v[4 * c + 1] = __uint_as_float(w.x & 0xffff0000u);
+      v[4 * c + 2] = __uint_as_float(w.y << 16);
+      v[4 * c + 3] = __uint_as_float(w.y & 0xffff0000u);
+    }
+  } else {
+    const float* xr = (const float*)p.x + in_row * p.ldx;
+#pragma unroll
+    for (int c = 0; c < nch; ++c) {
+      const f32x4 w = *(const f32x4*)(xr + c * 256 + lane * 4);
+      v[4 * c + 0] = w[0];
+      v[4 * c + 1] = w[1];
+      v[4 * c + 2] = w[2];
+      v[4 * c + 3] = w[3];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4 * nch; ++i) ss += v[i] * v[i];
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)D + p.eps);
+  const float* shift = p.shift ? p.shift + seg * p.mod_seg_stride : nullptr;
+  const float* scale = p.scale ? p.scale + seg * p.mod_seg_stride : nullptr;
+  bf16_t* yr = p.y + m * p.ldy;
+#pragma unroll
+  for (int c = 0; c < nch; ++c) {
+    const int n = c * 256 + lane * 4;
+    float o[4];
+    float wgt[4] = {1.f, 1.f, 1.f, 1.f};
+    if (p.w) {
+      const u32x2 ww = *(const u32x2*)(p.w + n);
+      wgt[0] = __uint_as_float(ww.x << 16);
+      wgt[1] = __uint_as_float(ww.x & 0xffff0000u);
+      wgt[2] = __uint_as_float(ww.y << 16);
+      wgt[3] = __uint_as_float(ww.y & 0xffff0000u);
+    }
+    f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    if (scale) sc = *(const f32x4*)(scale + n);
+    if (shift) sh = *(const f32x4*)(shift + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = v[4 * c + j] * r * wgt[j] * (1.f + sc[j]) + sh[j];
+    u32x2 st;
+    st.x = pack2bf(o[0], o[1]);
+    st.y = pack2bf(o[2], o[3]);
+    *(u32x2*)(yr + n) = st;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// RoPE (2-D, rotate-half pairs (j, j+128), rotation by -theta) + per-head RMSNorm (no weight), in place
+// on bf16 heads of 256. Reference: apply_rotary_emb (model.py:403-414) then QKNorm (model.py:115-126,180,197).
+// One wave per (row, head); lane l holds elements 4(l&31)+i of half (l>>5) -> the rotation partner is
+// lane l^32.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rope_qknorm_kernel(RopeNormParams p) {
+  const int lane = threadIdx.x & 63;
+  const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long total = (long)p.rows * p.heads;
+  if (item >= total) return;
+  const long row = item / p.heads;
+  const int head = (int)(item % p.heads);
+  bf16_t* xp = p.x + row * p.ldx + (long)head * 256 + lane * 4;
+  const u32x2 w = *(const u32x2*)xp;
+  float v[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                __uint_as_float(w.y & 0xffff0000u)};
+  if (p.cos != nullptr && head < p.rope_heads) {
+    const long tok = row % p.tokens_per_seq;
+    const int j = 4 * (lane & 31);
+    const f32x4 c = *(const f32x4*)(p.cos + tok * 128 + j);
+    const f32x4 s = *(const f32x4*)(p.sin + tok * 128 + j);
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float partner = __shfl_xor(v[i], 32, 64);
+      // lanes < 32 hold x1 (y1 = x1 c + x2 s); lanes >= 32 hold x2 (y2 = -x1 s + x2 c)
+      o[i] = (lane < 32) ? (v[i] * c[i] + partner * s[i]) : (-partner * s[i] + v[i] * c[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = o[i];
+  }
+  float ss = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss * (1.f / 256.f) + p.eps);
+  u32x2 st;
+  st.x = pack2bf(v[0] * r, v[1] * r);
+  st.y = pack2bf(v[2] * r, v[3] * r);
+  *(u32x2*)xp = st;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Patchify (PatchEmbed conv k=s=p as a GEMM, model.py:318-331): latents [Bi, C, H, W] (fp32 or bf16)
+// -> patches bf16 [dup*Bi*(H/p)*(W/p), C*p*p] with columns in (c, p1, p2) order (= conv weight layout).
+// Copy `d` of image i lands at batch index d*Bi + i (CFG batch = cat([latents]*2), pipeline.py:264).
+// ------------------------------------------------------------------------------------------------
+template <bool IN_BF16>
+__global__ __launch_bounds__(256) void patchify_kernel(const void* lat, bf16_t* out, int Bi, int C, int H, int W,
+                                                       int P, int dup) {
+  const int hp = H / P, wp = W / P;
+  const int K = C * P * P;
+  const long total = (long)dup * Bi * hp * wp * K;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(idx % K);
+    const long row = idx / K;
+    const int x = (int)(row % wp);
+    const int y = (int)((row / wp) % hp);
+    const long b = row / ((long)wp * hp);
+    const int i = (int)(b % Bi);
+    const int c = k / (P * P);
+    const int p1 = (k / P) % P;
+    const int p2 = k % P;
+    const long src = (((long)i * C + c) * H + (y * P + p1)) * W + (x * P + p2);
+    float v;
+    if constexpr (IN_BF16)
+      v = bf2f(((const bf16_t*)lat)[src]);
+    else
+      v = ((const float*)lat)[src];
+    out[idx] = f2bf(v);
+  }
+}
+
+// register tokens into rows [0, R) of every sequence of the fp32 residual stream
+__global__ __launch_bounds__(256) void fill_registers_kernel(float* x, const bf16_t* reg, int B, int T, int R,
+                                                             int D) {
+  const long total = (long)B * R * D;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(idx % D);
+    const long r = (idx / D) % R;
+    const long b = idx / ((long)D * R);
+    x[(b * T + r) * D + d] = bf2f(reg[r * D + d]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Unpatchify + classifier-free guidance + Euler update (pipeline.py:274,290,296-297; model.py:583-590).
+//   out rows = [dup*Bi*HW, C*p*p] fp32 with columns (p1, p2, c); image i uses rows of copy 0 (uncond)
+//   and copy 1 (cond): v = u + g (c - u); acc[i] += dt * v  (fp32 accumulator, [Bi, C, H, W])
+// With guidance disabled (dup == 1) v = out.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cfg_euler_kernel(const float* out, float* acc, int Bi, int C, int H, int W,
+                                                        int P, int dup, float g, float dt) {
+  const int hp = H / P, wp = W / P;
+  const long HW = (long)hp * wp;
+  const long total = (long)Bi * C * H * W;
+  const int K = C * P * P;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(idx % W);
+    const int y = (int)((idx / W) % H);
+    const int c = (int)((idx / ((long)W * H)) % C);
+    const long i = idx / ((long)W * H * C);
+    const long prow = (long)(y / P) * wp + (x / P);
+    const int col = ((y % P) * P + (x % P)) * C + c;
+    float v;
+    if (dup == 2) {
+      const float u = out[(i * HW + prow) * K + col];
+      const float cc = out[((Bi + i) * HW + prow) * K + col];
+      v = u + g * (cc - u);
+    } else {
+      v = out[(i * HW + prow) * K + col];
+    }
+    acc[idx] += dt * v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Adaptive projected guidance (APG, pipeline.py:276-287) + Euler update. The reference reduces over the
+// WHOLE batch tensor, so one 1024-thread workgroup does the three passes (sums, std, update) in-launch.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float block_sum_1024(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = (threadIdx.x < 16) ? red[threadIdx.x] : 0.f;
+  if (w == 0) t = wave_sum(t);
+  if (threadIdx.x == 0) red[16] = t;
+  __syncthreads();
+  return red[16];
+}
+
+__global__ __launch_bounds__(1024) void apg_euler_kernel(const float* out, float* acc, int Bi, int C, int H, int W,
+                                                         int P, float g, float thr, float dt) {
+  __shared__ float red[32];
+  const int wp = W / P;
+  const long HW = (long)(H / P) * wp;
+  const long n = (long)Bi * C * H * W;
+  const int K = C * P * P;
+  auto uc = [&](long idx, float& u, float& c) {
+    const int x = (int)(idx % W);
+    const int y = (int)((idx / W) % H);
+    const int ch = (int)((idx / ((long)W * H)) % C);
+    const long i = idx / ((long)W * H * C);
+    const long prow = (long)(y / P) * wp + (x / P);
+    const int col = ((y % P) * P + (x % P)) * C + ch;
+    u = out[(i * HW + prow) * K + col];
+    c = out[((Bi + i) * HW + prow) * K + col];
+  };
+  float s_dd = 0.f, s_yy = 0.f;
+  for (long idx = threadIdx.x; idx < n; idx += blockDim.x) {
+    float u, c;
+    uc(idx, u, c);
+    s_dd += c * (c - u);
+    s_yy += c * c;
+  }
+  const float dydd = block_sum_1024(s_dd, red);
+  const float dyy = block_sum_1024(s_yy, red);
+  const float k = dyy > 0.f ? dydd / dyy : 0.f;
+  float s1 = 0.f, s2 = 0.f;
+  for (long idx = threadIdx.x; idx < n; idx += blockDim.x) {
+    float u, c;
+    uc(idx, u, c);
+    const float o = (c - u) - k * c;
+    s1 += o;
+    s2 += o * o;
+  }
+  const float so = block_sum_1024(s1, red);
+  const float soo = block_sum_1024(s2, red);
+  const float mean = so / (float)n;
+  const float var = n > 1 ? fmaxf(soo - mean * so, 0.f) / (float)(n - 1) : 0.f;
+  const float sd = sqrtf(var);
+  const float sc = sd > 0.f ? fminf(1.f, thr / sd) : 1.f;
+  for (long idx = threadIdx.x; idx < n; idx += blockDim.x) {
+    float u, c;
+    uc(idx, u, c);
+    const float o = (c - u) - k * c;
+    acc[idx] += dt * (c + (g - 1.f) * sc * o);
+  }
+}
+
+// unpatchify only (DiT.forward output, model.py:583-590): out rows [B*HW, C*p*p] -> y [B, C, H, W]
+template <bool OUT_BF16>
+__global__ __launch_bounds__(256) void unpatchify_kernel(const float* out, void* y, int B, int C, int H, int W,
+                                                         int P) {
+  const int hp = H / P, wp = W / P;
+  const long HW = (long)hp * wp;
+  const long total = (long)B * C * H * W;
+  const int K = C * P * P;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(idx % W);
+    const int yy = (int)((idx / W) % H);
+    const int c = (int)((idx / ((long)W * H)) % C);
+    const long i = idx / ((long)W * H * C);
+    const long prow = (long)(yy / P) * wp + (x / P);
+    const int col = ((yy % P) * P + (x % P)) * C + c;
+    const float v = out[(i * HW + prow) * K + col];
+    if constexpr (OUT_BF16)
+      ((bf16_t*)y)[idx] = f2bf(v);
+    else
+      ((float*)y)[idx] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Timestep embedding (model.py:20-28, 551) with the reference bf16 quantisation of the bf16 pipeline:
+//   t_q = bf16(bf16(t) * 1000) (pipeline.py:260 + model.py:551), emb = [cos(t_q f), sin(t_q f)], f_j =
+//   exp(-ln(1e4) j / half); the embedding is cast to bf16 (model.py:551 .to(dtype)).
+// quantize = 0 reproduces the fp32 model (t * 1000 in fp32).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void timestep_embed_kernel(const float* t, bf16_t* emb, int n, int D,
+                                                             int quantize) {
+  const int half = D / 2;
+  const long total = (long)n * D;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(idx % D);
+    const long i = idx / D;
+    float tv = t[i];
+    if (quantize) {
+      tv = bf2f(f2bf(tv));
+      tv = bf2f(f2bf(tv * 1000.f));
+    } else {
+      tv = tv * 1000.f;
+    }
+    const int jj = j < half ? j : j - half;
+    const float freq = expf(-9.210340371976184f * (float)jj / (float)half);
+    const float a = tv * freq;
+    emb[idx] = f2bf(j < half ? cosf(a) : sinf(a));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// 2-D RoPE tables (TwoDimRotary, model.py:334-386): rows [0, R) are registers (cos 1, sin 0); token
+// R + y*w + x gets cat(y * inv_freq, x * inv_freq); values rounded to bf16 when the model is bf16
+// (buffers are cast by .to(bf16)). inv_freq (64 fp32) comes from the host (double math).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rope_table_kernel(const float* inv_freq, float* cos_t, float* sin_t, int hh,
+                                                         int ww, int R, int round_bf16) {
+  const long total = (long)(R + hh * ww) * 128;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(idx % 128);
+    const long tok = idx / 128;
+    float c = 1.f, s = 0.f;
+    if (tok >= R) {
+      const long q = tok - R;
+      const int y = (int)(q / ww), x = (int)(q % ww);
+      const float pos = j < 64 ? (float)y : (float)x;
+      const float a = pos * inv_freq[j & 63];
+      c = cosf(a);
+      s = sinf(a);
+      if (round_bf16) {
+        c = bf2f(f2bf(c));
+        s = bf2f(f2bf(s));
+      }
+    }
+    cos_t[idx] = c;
+    sin_t[idx] = s;
+  }
+}
+
+// gather rows (context compaction by the attention mask, model.py:31-64)
+__global__ __launch_bounds__(256) void gather_rows_kernel(const bf16_t* src, bf16_t* dst, const int* idx, long n,
+                                                          int cols) {
+  const long total = n * cols / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / (cols / 8);
+    const int c = (int)(i % (cols / 8));
+    ((u32x4*)dst)[r * (cols / 8) + c] = ((const u32x4*)src)[(long)idx[r] * (cols / 8) + c];
+  }
+}
+
+int grid_for(long total, int per_block = 256) {
+  long g = (total + per_block - 1) / per_block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
+  FLITE_REQUIRE(p.ldx % 4 == 0 && p.ldy % 4 == 0, "rmsnorm: strides must be multiples of 4");
+  if (p.rows <= 0) return 0;
+  const int grid = (int)((p.rows + 3) / 4);
+#define FLITE_NORM_CASE(N)                                                                       \
+  case N:                                                                                        \
+    if (in_bf16)                                                                                 \
+      hipLaunchKernelGGL((rmsnorm_mod_kernel<true, N>), dim3(grid), dim3(256), 0, s, p);         \
+    else                                                                                         \
+      hipLaunchKernelGGL((rmsnorm_mod_kernel<false, N>), dim3(grid), dim3(256), 0, s, p);        \
+    break;
+  FLITE_REQUIRE(p.D % 256 == 0, "rmsnorm: D must be a multiple of 256");
+  switch (p.D / 256) {
+    FLITE_NORM_CASE(1)
+    FLITE_NORM_CASE(2)
+    FLITE_NORM_CASE(3)
+    FLITE_NORM_CASE(4)
+    FLITE_NORM_CASE(6)
+    FLITE_NORM_CASE(8)
+    FLITE_NORM_CASE(12)
+    FLITE_NORM_CASE(16)
+    default:
+      FLITE_REQUIRE(false, "rmsnorm: unsupported D (256 x {1,2,3,4,6,8,12,16})");
+  }
+#undef FLITE_NORM_CASE
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int rope_qknorm(const RopeNormParams& p, hipStream_t s) {
+  FLITE_REQUIRE(p.ldx % 4 == 0, "rope_qknorm: stride must be a multiple of 4");
+  if (p.cos) FLITE_REQUIRE(p.tokens_per_seq > 0, "rope_qknorm: tokens_per_seq must be > 0");
+  const long items = (long)p.rows * p.heads;
+  if (items <= 0) return 0;
+  hipLaunchKernelGGL(rope_qknorm_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, p);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int patchify(const void* lat, bool in_bf16, bf16_t* out, int Bi, int C, int H, int W, int P, int dup,
+             hipStream_t s) {
+  const long total = (long)dup * Bi * C * H * W;
+  if (in_bf16)
+    hipLaunchKernelGGL(patchify_kernel<true>, dim3(grid_for(total)), dim3(256), 0, s, lat, out, Bi, C, H, W, P, dup);
+  else
+    hipLaunchKernelGGL(patchify_kernel<false>, dim3(grid_for(total)), dim3(256), 0, s, lat, out, Bi, C, H, W, P,
+                       dup);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int fill_registers(float* x, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s) {
+  hipLaunchKernelGGL(fill_registers_kernel, dim3(grid_for((long)B * R * D)), dim3(256), 0, s, x, reg, B, T, R, D);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int cfg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, int dup, float g, float dt,
+              hipStream_t s) {
+  hipLaunchKernelGGL(cfg_euler_kernel, dim3(grid_for((long)Bi * C * H * W)), dim3(256), 0, s, out, acc, Bi, C, H,
+                     W, P, dup, g, dt);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, float g, float thr, float dt,
+              hipStream_t s) {
+  hipLaunchKernelGGL(apg_euler_kernel, dim3(1), dim3(1024), 0, s, out, acc, Bi, C, H, W, P, g, thr, dt);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int unpatchify(const float* out, void* y, bool out_bf16, int B, int C, int H, int W, int P, hipStream_t s) {
+  const long total = (long)B * C * H * W;
+  if (out_bf16)
+    hipLaunchKernelGGL(unpatchify_kernel<true>, dim3(grid_for(total)), dim3(256), 0, s, out, y, B, C, H, W, P);
+  else
+    hipLaunchKernelGGL(unpatchify_kernel<false>, dim3(grid_for(total)), dim3(256), 0, s, out, y, B, C, H, W, P);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int timestep_embed(const float* t, bf16_t* emb, int n, int D, int quantize, hipStream_t s) {
+  FLITE_REQUIRE(D % 2 == 0, "timestep_embed: D must be even");
+  hipLaunchKernelGGL(timestep_embed_kernel, dim3(grid_for((long)n * D)), dim3(256), 0, s, t, emb, n, D, quantize);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int rope_table(const float* inv_freq, float* cos_t, float* sin_t, int hh, int ww, int R, int round_bf16,
+               hipStream_t s) {
+  const long total = (long)(R + hh * ww) * 128;
+  hipLaunchKernelGGL(rope_table_kernel, dim3(grid_for(total)), dim3(256), 0, s, inv_freq, cos_t, sin_t, hh, ww, R,
+                     round_bf16);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gather_rows(const bf16_t* src, bf16_t* dst, const int* idx, long n, int cols, hipStream_t s) {
+  FLITE_REQUIRE(cols % 8 == 0, "gather_rows: cols must be a multiple of 8");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(n * cols / 8)), dim3(256), 0, s, src, dst, idx, n, cols);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace flite

@@ -1,0 +1,110 @@
+// Internal launcher declarations for the gfx950 kernels (host side). Not part of the C ABI.
+#pragma once
+#include "common.h"
+
+namespace flite {
+
+enum GemmEpilogue {
+  EPI_STORE_BF16 = 0,   // out_bf16[m][n] = acc + bias[n]
+  EPI_STORE_F32 = 1,    // out_f32[m][n]  = acc + bias[n]
+  EPI_RESID_F32 = 2,    // out_f32[m][n] += gate[seg(m)][n] * (acc + bias[n])   (gated residual, model.py:289,297,301)
+  EPI_SWIGLU_BF16 = 3,  // out_bf16[m][f] = silu(A.Wg[f]) * (A.Wu[f])            (LigerSwiGLUMLP gate/up)
+};
+
+struct GemmParams {
+  const bf16_t* A = nullptr;  // [M, K], row stride lda (elements)
+  long lda = 0;
+  const bf16_t* W = nullptr;  // [N, K], row stride ldw (nn.Linear weight)
+  long ldw = 0;
+  const bf16_t* W2 = nullptr;    // SwiGLU only: up_proj weight [F, K]; W = gate_proj, N = 2F
+  const bf16_t* bias = nullptr;  // [N] bf16 (model parameter dtype) or null
+  void* out = nullptr;           // output, row stride ldo (elements)
+  long ldo = 0;
+  const float* gate = nullptr;   // RESID: gate rows, one per segment of rows_per_seg rows
+  long gate_seg_stride = 0;      // elements between consecutive segments' gate rows (0 = shared)
+  int rows_per_seg = 1;
+  int M = 0, N = 0, K = 0;
+  int act = 0;                   // 1: SiLU after bias (time_embed / adaLN inputs, model.py:448-456)
+  // output row mapping: out_row = (m / out_seg) * out_seg_stride + out_seg_off + m % out_seg (0 = identity)
+  long out_seg = 0, out_seg_stride = 0, out_seg_off = 0;
+};
+
+int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream);
+
+// Varlen flash attention (flash_attn_varlen_func semantics, non-causal). Token t of sequence b lives at
+// row cu[b] + t; head h of a row starts at h * head_stride elements.
+struct AttnParams {
+  const bf16_t* q = nullptr;
+  const bf16_t* k = nullptr;
+  const bf16_t* v = nullptr;
+  bf16_t* o = nullptr;
+  long q_row_stride = 0, k_row_stride = 0, v_row_stride = 0, o_row_stride = 0;
+  long q_head_stride = 0, k_head_stride = 0, v_head_stride = 0, o_head_stride = 0;
+  const int* cu_q = nullptr;  // device int32 [B+1]
+  const int* cu_k = nullptr;  // device int32 [B+1]
+  int B = 0, H = 0, head_dim = 0;
+  int max_q = 0;              // max query length (grid size)
+  float scale = 1.f;
+};
+
+int attn_fwd(const AttnParams& p, hipStream_t stream);
+
+}  // namespace flite
+
+namespace flite {
+
+struct NormModParams {
+  const void* x = nullptr;  // fp32 or bf16 input rows
+  long ldx = 0;
+  bf16_t* y = nullptr;      // bf16 output rows
+  long ldy = 0;
+  const bf16_t* w = nullptr;  // norm weight [D] (bf16 param) or null
+  const float* shift = nullptr;  // modulation rows (fp32), one per segment, or null
+  const float* scale = nullptr;
+  long mod_seg_stride = 0;
+  long rows = 0;
+  int D = 0;
+  float eps = 1e-6f;
+  // input row mapping: in_row = (m / in_seg) * in_stride + in_off + m % in_seg (in_seg = 0: identity);
+  // the modulation segment of output row m is m / in_seg (0 when in_seg == 0)
+  long in_seg = 0, in_stride = 0, in_off = 0;
+};
+int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s);
+
+struct RopeNormParams {
+  bf16_t* x = nullptr;  // rows of heads (256 wide each), in place
+  long ldx = 0;
+  long rows = 0;
+  int heads = 0;         // heads per row processed (starting at column 0)
+  int rope_heads = 0;    // heads [0, rope_heads) get RoPE (q and k of self-attention), the rest norm only
+  const float* cos = nullptr;  // [tokens_per_seq, 128] or null (no RoPE)
+  const float* sin = nullptr;
+  long tokens_per_seq = 0;
+  float eps = 1e-6f;
+};
+int rope_qknorm(const RopeNormParams& p, hipStream_t s);
+
+int patchify(const void* lat, bool in_bf16, bf16_t* out, int Bi, int C, int H, int W, int P, int dup, hipStream_t s);
+int fill_registers(float* x, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s);
+int cfg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, int dup, float g, float dt,
+              hipStream_t s);
+int unpatchify(const float* out, void* y, bool out_bf16, int B, int C, int H, int W, int P, hipStream_t s);
+int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, float g, float thr, float dt,
+              hipStream_t s);
+int timestep_embed(const float* t, bf16_t* emb, int n, int D, int quantize, hipStream_t s);
+int rope_table(const float* inv_freq, float* cos_t, float* sin_t, int hh, int ww, int R, int round_bf16,
+               hipStream_t s);
+int gather_rows(const bf16_t* src, bf16_t* dst, const int* idx, long n, int cols, hipStream_t s);
+
+}  // namespace flite
+
+namespace flite {
+int gemm_init();  // set kernel attributes once (outside any graph capture)
+int attn_init();
+}  // namespace flite
+
+namespace flite {
+uint64_t fnv1a64(const char* s);
+int hash_init(void* out, int out_bf16, long n, const char* name, uint64_t seed, double std, hipStream_t s);
+int fill_bf16(bf16_t* out, long n, float v, hipStream_t s);
+}  // namespace flite

@@ -1,0 +1,296 @@
+"""ctypes binding of libflite_hip.so (the C ABI in include/flite.h).
+
+This is the ONLY compute path of the package: there is no CPU or PyTorch fallback. If the library is
+missing, or a tensor is not on a ROCm device, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_LIB_PATH = Path(__file__).resolve().parent / "libflite_hip.so"
+_lib = None
+
+EPI_STORE_BF16 = 0
+EPI_STORE_F32 = 1
+EPI_RESID_F32 = 2
+EPI_SWIGLU_BF16 = 3
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_l = ctypes.c_long
+_f = ctypes.c_float
+_d = ctypes.c_double
+_cp = ctypes.c_char_p
+_ull = ctypes.c_ulonglong
+
+
+class DitConfig(ctypes.Structure):
+    """flite_dit_config (include/flite.h)."""
+
+    _fields_ = [
+        ("in_channels", _i),
+        ("patch_size", _i),
+        ("hidden_size", _i),
+        ("depth", _i),
+        ("num_heads", _i),
+        ("mlp_hidden", _i),
+        ("cross_attn_input_size", _i),
+        ("train_bias_and_rms", _i),
+        ("per_block_adaln", _i),
+        ("n_register_tokens", _i),
+        ("rope_base", _f),
+        ("bf16_timestep_quant", _i),
+        ("bf16_rope_tables", _i),
+    ]
+
+
+# name -> (restype, argtypes); every symbol declared in include/flite.h
+SIGNATURES = {
+    "flite_last_error": (_cp, []),
+    "flite_version": (_i, []),
+    "flite_gemm_bf16": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _vp, _i, _vp, _l, _vp, _l, _i]),
+    "flite_attn_varlen_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _f]),
+    "flite_rmsnorm_modulate": (_i, [_vp, _vp, _i, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
+    "flite_rope_qknorm": (_i, [_vp, _vp, _l, _l, _i, _i, _vp, _vp, _l, _f]),
+    "flite_gather_rows": (_i, [_vp, _vp, _vp, _vp, _l, _i]),
+    "flite_rope_tables": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _i]),
+    "flite_timestep_embedding": (_i, [_vp, _vp, _vp, _i, _i, _i]),
+    "flite_init_param": (_i, [_vp, _vp, _i, _l, _cp, _ull, _d, _i]),
+    "flite_dit_create": (_i, [ctypes.POINTER(DitConfig), ctypes.POINTER(_vp)]),
+    "flite_dit_destroy": (_i, [_vp]),
+    "flite_dit_bind": (_i, [_vp, _cp, _vp, _l]),
+    "flite_dit_prepare": (_i, [_vp, _i, _i, _i, _i, _i]),
+    "flite_dit_set_context": (_i, [_vp, _vp, _vp, ctypes.POINTER(_i), _i]),
+    "flite_dit_set_timesteps": (_i, [_vp, _vp, _vp, _i, _i]),
+    "flite_dit_forward": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _i]),
+    "flite_dit_sample": (_i, [_vp, _vp, _vp, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _f, _i, _i, _f, _i]),
+}
+
+
+class FliteError(RuntimeError):
+    pass
+
+
+def lib_path() -> Path:
+    return Path(os.environ.get("FLITE_LIB", str(_LIB_PATH)))
+
+
+def load():
+    """Load libflite_hip.so and bind every exported entry point. Raises if the library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not path.exists():
+        raise FliteError(
+            f"libflite_hip.so not found at {path}; build it with `python f-lite_amd/build_native.py` "
+            "(there is no CPU fallback)"
+        )
+    lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str):
+    if status != 0:
+        msg = load().flite_last_error().decode(errors="replace")
+        raise FliteError(f"{what} failed ({status}): {msg}")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu(t: torch.Tensor, name: str, dtype=None, contiguous=True):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        dev = t.device if isinstance(t, torch.Tensor) else type(t)
+        raise FliteError(f"{name}: tensor must live on a ROCm device (got {dev}); there is no CPU fallback")
+    if dtype is not None and t.dtype != dtype:
+        raise FliteError(f"{name}: expected {dtype}, got {t.dtype}")
+    if contiguous and not t.is_contiguous():
+        raise FliteError(f"{name}: tensor must be contiguous")
+    return t.data_ptr()
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+# ------------------------------------------------------------------------------------------------
+# kernel-level operators
+# ------------------------------------------------------------------------------------------------
+def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, *, out=None, epilogue=EPI_STORE_BF16, w2=None,
+         gate=None, gate_seg_stride=0, rows_per_seg=1) -> torch.Tensor:
+    """C = a . w^T (+bias) with the selected fused epilogue. a:[M,K] bf16, w:[N,K] bf16 (nn.Linear layout)."""
+    lib = load()
+    M, K = a.shape
+    N = w.shape[0]
+    if a.stride(1) != 1 or w.stride(1) != 1:
+        raise FliteError("gemm: operands must be K-contiguous")
+    if epilogue == EPI_SWIGLU_BF16:
+        if w2 is None or w2.shape != w.shape:
+            raise FliteError("gemm(swiglu): w2 must match w")
+        Nv = 2 * N
+        if out is None:
+            out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
+    else:
+        Nv = N
+        if out is None:
+            dt = torch.bfloat16 if epilogue == EPI_STORE_BF16 else torch.float32
+            out = torch.empty(M, N, device=a.device, dtype=dt)
+    require_gpu(a, "a", torch.bfloat16, contiguous=False)
+    require_gpu(w, "w", torch.bfloat16, contiguous=False)
+    require_gpu(out, "out", contiguous=False)
+    if bias is not None:
+        require_gpu(bias, "bias", torch.bfloat16)
+    st = lib.flite_gemm_bf16(
+        stream_ptr(a.device), M, Nv, K, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), _ptr(w2),
+        _ptr(bias), epilogue, out.data_ptr(), out.stride(0), _ptr(gate), gate_seg_stride, rows_per_seg,
+    )
+    check(st, "flite_gemm_bf16")
+    return out
+
+
+def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None):
+    """flash_attn_varlen_func replacement: q [Lq, h, 256], k/v [Lk, h, 256] (row-major, any row stride)."""
+    lib = load()
+    Lq, H, D = q.shape
+    if out is None:
+        out = torch.empty(Lq, H, D, device=q.device, dtype=torch.bfloat16)
+    for t, n in ((q, "q"), (k, "k"), (v, "v"), (out, "out")):
+        require_gpu(t, n, torch.bfloat16, contiguous=False)
+        if t.stride(2) != 1 or t.stride(1) != D:
+            raise FliteError(f"attn: {n} must be [L, h, d] with contiguous heads")
+    require_gpu(cu_q, "cu_q", torch.int32)
+    require_gpu(cu_k, "cu_k", torch.int32)
+    st = lib.flite_attn_varlen_fwd(stream_ptr(q.device), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(),
+                                   q.stride(0), k.stride(0), v.stride(0), out.stride(0), D, cu_q.data_ptr(),
+                                   cu_k.data_ptr(), cu_q.numel() - 1, H, D, max_q, scale)
+    check(st, "flite_attn_varlen_fwd")
+    return out
+
+
+def rmsnorm_modulate(x, w=None, shift=None, scale=None, seg_rows=0, eps=1e-6, out=None):
+    lib = load()
+    rows, dim = x.shape
+    if out is None:
+        out = torch.empty(rows, dim, device=x.device, dtype=torch.bfloat16)
+    require_gpu(x, "x", contiguous=False)
+    st = lib.flite_rmsnorm_modulate(stream_ptr(x.device), x.data_ptr(), int(x.dtype == torch.bfloat16), x.stride(0),
+                                    out.data_ptr(), out.stride(0), _ptr(w), _ptr(shift), _ptr(scale),
+                                    shift.stride(0) if shift is not None and shift.dim() == 2 else 0, seg_rows, rows,
+                                    dim, eps)
+    check(st, "flite_rmsnorm_modulate")
+    return out
+
+
+def rope_qknorm_(x, heads, rope_heads, cos=None, sin=None, tokens_per_seq=0, eps=1e-6):
+    lib = load()
+    require_gpu(x, "x", torch.bfloat16, contiguous=False)
+    st = lib.flite_rope_qknorm(stream_ptr(x.device), x.data_ptr(), x.stride(0), x.shape[0], heads, rope_heads,
+                               _ptr(cos), _ptr(sin), tokens_per_seq, eps)
+    check(st, "flite_rope_qknorm")
+    return x
+
+
+def rope_tables(h, w, n_reg=16, base=10000.0, round_bf16=True, device="cuda"):
+    lib = load()
+    cos = torch.empty(n_reg + h * w, 128, device=device, dtype=torch.float32)
+    sin = torch.empty_like(cos)
+    check(lib.flite_rope_tables(stream_ptr(cos.device), cos.data_ptr(), sin.data_ptr(), h, w, n_reg, base,
+                                int(round_bf16)), "flite_rope_tables")
+    return cos, sin
+
+
+def timestep_embedding(t, dim, quantize):
+    lib = load()
+    require_gpu(t, "t", torch.float32)
+    emb = torch.empty(t.numel(), dim, device=t.device, dtype=torch.bfloat16)
+    check(lib.flite_timestep_embedding(stream_ptr(t.device), t.data_ptr(), emb.data_ptr(), t.numel(), dim,
+                                       int(quantize)), "flite_timestep_embedding")
+    return emb
+
+
+def init_param_(t: torch.Tensor, name: str, seed: int = 0, std: float = 0.02, ones: bool = False):
+    """Fill t in place with the deterministic generator (bit-identical to oracle/weights.py)."""
+    lib = load()
+    require_gpu(t, name)
+    if t.dtype not in (torch.bfloat16, torch.float32):
+        raise FliteError("init_param: bf16 or fp32 only")
+    check(lib.flite_init_param(stream_ptr(t.device), t.data_ptr(), int(t.dtype == torch.bfloat16), t.numel(),
+                               name.encode(), seed, std, int(ones)), "flite_init_param")
+    return t
+
+
+def gather_rows(src, idx, out=None):
+    lib = load()
+    n = idx.numel()
+    if out is None:
+        out = torch.empty(n, src.shape[1], device=src.device, dtype=src.dtype)
+    require_gpu(src, "src", torch.bfloat16)
+    require_gpu(idx, "idx", torch.int32)
+    check(lib.flite_gather_rows(stream_ptr(src.device), src.data_ptr(), out.data_ptr(), idx.data_ptr(), n,
+                                src.shape[1]), "flite_gather_rows")
+    return out
+
+
+class DitEngine:
+    """Owner of a native flite_dit handle (the DiT forward and the denoise loop in C++)."""
+
+    def __init__(self, cfg: DitConfig):
+        self.lib = load()
+        self.h = _vp()
+        check(self.lib.flite_dit_create(ctypes.byref(cfg), ctypes.byref(self.h)), "flite_dit_create")
+        self.cfg = cfg
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.flite_dit_destroy(self.h)
+        except Exception:
+            pass
+
+    def bind(self, name: str, t: torch.Tensor):
+        require_gpu(t, name, torch.bfloat16)
+        check(self.lib.flite_dit_bind(self.h, name.encode(), t.data_ptr(), t.numel()), f"bind({name})")
+
+    def prepare(self, batch, lat_h, lat_w, n_ctx, n_t):
+        check(self.lib.flite_dit_prepare(self.h, batch, lat_h, lat_w, n_ctx, n_t), "flite_dit_prepare")
+
+    def set_context(self, ctx_packed: torch.Tensor, cu_host):
+        require_gpu(ctx_packed, "context", torch.bfloat16)
+        arr = (_i * len(cu_host))(*cu_host)
+        check(self.lib.flite_dit_set_context(self.h, stream_ptr(ctx_packed.device), ctx_packed.data_ptr(), arr,
+                                             len(cu_host) - 1), "flite_dit_set_context")
+
+    def set_timesteps(self, t: torch.Tensor, quantize: bool):
+        require_gpu(t, "timesteps", torch.float32)
+        check(self.lib.flite_dit_set_timesteps(self.h, stream_ptr(t.device), t.data_ptr(), t.numel(), int(quantize)),
+              "flite_dit_set_timesteps")
+
+    def forward(self, x: torch.Tensor, out: torch.Tensor, t_row0=0, t_row_step=1):
+        require_gpu(x, "x")
+        require_gpu(out, "out")
+        check(self.lib.flite_dit_forward(self.h, stream_ptr(x.device), x.data_ptr(), int(x.dtype == torch.bfloat16),
+                                         x.shape[0], t_row0, t_row_step, out.data_ptr(),
+                                         int(out.dtype == torch.bfloat16)), "flite_dit_forward")
+        return out
+
+    def sample(self, acc: torch.Tensor, n_img, t_list, dt_list, guidance, use_cfg, apg=False, apg_thr=0.03,
+               use_graph=True):
+        require_gpu(acc, "latents", torch.float32)
+        n = len(t_list)
+        ta = (_f * n)(*t_list)
+        da = (_f * n)(*dt_list)
+        check(self.lib.flite_dit_sample(self.h, stream_ptr(acc.device), acc.data_ptr(), n_img, n, ta, da,
+                                        float(guidance), int(use_cfg), int(apg), float(apg_thr), int(use_graph)),
+              "flite_dit_sample")
+        return acc

@@ -1,0 +1,149 @@
+/*
+ * flite.h -- C ABI of libflite_hip.so, the MI355X (gfx950) native F-Lite sampling path.
+ *
+ * Conventions (all entry points):
+ *   - Buffers are caller-owned DEVICE memory (e.g. torch .data_ptr()); sizes are element counts.
+ *   - `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream).
+ *   - Return 0 on success, non-zero on error; the message is available from flite_last_error()
+ *     (thread-local). Nothing throws across this boundary.
+ *   - No allocation and no host synchronisation inside the launch entry points (hipGraph-capturable).
+ *   - bf16 tensors are passed as their 16-bit storage; fp32 as float.
+ *
+ * Each entry point cites the reference interface it replaces (sippycoder/f-lite @ /root/reference).
+ */
+#ifndef FLITE_H_
+#define FLITE_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLITE_ABI_VERSION 1
+
+/* Thread-local message of the last failing call. */
+const char* flite_last_error(void);
+int flite_version(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Kernel-level operators (what the native library replaces under f_lite/model.py)
+ * ------------------------------------------------------------------------------------------- */
+
+/* Epilogue selectors for flite_gemm_bf16. */
+#define FLITE_EPI_STORE_BF16 0  /* out_bf16[m][n]  = A.W^T + bias                                  */
+#define FLITE_EPI_STORE_F32 1   /* out_f32[m][n]   = A.W^T + bias                                  */
+#define FLITE_EPI_RESID_F32 2   /* out_f32[m][n]  += gate[m/rows_per_seg][n] * (A.W^T + bias)      */
+#define FLITE_EPI_SWIGLU_BF16 3 /* out_bf16[m][f]  = silu(A.Wg^T)[f] * (A.Wu^T)[f], N = 2F          */
+
+/*
+ * bf16 GEMM with fused epilogue: C[M,N] = A[M,K] . W[N,K]^T  (W in nn.Linear [out,in] layout).
+ * Replaces nn.Linear (f_lite/model.py:151,153-156,436,448-456,472-475) and LigerSwiGLUMLP
+ * (model.py:261-267, SWIGLU: W = gate_proj.weight, W2 = up_proj.weight); the gated-residual
+ * epilogue fuses `x + f(n) * gate` (model.py:289,297,301). K % 64 == 0; lda, ldw % 8 == 0.
+ */
+int flite_gemm_bf16(void* stream, int M, int N, int K, const void* A, long lda, const void* W, long ldw,
+                    const void* W2, const void* bias, int epilogue, void* out, long ldo, const float* gate,
+                    long gate_seg_stride, int rows_per_seg);
+
+/*
+ * Varlen flash-attention forward, head_dim 256, non-causal.
+ * Replaces flash_attn_interface.flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
+ * max_seqlen_k, softmax_scale) (f_lite/model.py:203-210). Token t of sequence b is row cu[b]+t; head h of
+ * a row starts at h*head_stride. cu_seqlens_* are device int32 [B+1]. Output o has the q layout.
+ */
+int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void* v, void* o, long q_row_stride,
+                          long k_row_stride, long v_row_stride, long o_row_stride, long head_stride,
+                          const int* cu_seqlens_q, const int* cu_seqlens_k, int batch, int num_heads,
+                          int head_dim, int max_seqlen_q, float softmax_scale);
+
+/*
+ * RMSNorm (+weight) (+adaLN modulate) to bf16: y = x*rsqrt(mean(x^2)+eps) * w * (1+scale) + shift.
+ * Replaces LigerRMSNorm (model.py:238,248,260,437), RMSNorm (model.py:92-108) and the modulate
+ * `norm_x * (1 + scale) + shift` (model.py:284,293,300,580). x is fp32 (x_is_bf16 = 0) or bf16.
+ * shift/scale are fp32 rows, one per segment of seg_rows rows (seg_rows = 0: single segment), may be NULL.
+ */
+int flite_rmsnorm_modulate(void* stream, const void* x, int x_is_bf16, long ldx, void* y, long ldy, const void* w,
+                           const float* shift, const float* scale, long mod_seg_stride, long seg_rows, long rows,
+                           int dim, float eps);
+
+/*
+ * In-place 2-D RoPE (rotate-half, model.py:403-414) on heads [0, rope_heads) followed by the per-head
+ * RMSNorm of QKNorm (model.py:115-126) on heads [0, heads) of bf16 rows (head size 256).
+ * cos/sin: fp32 [tokens_per_seq, 128] tables (NULL = no RoPE); row r uses table row r % tokens_per_seq.
+ */
+int flite_rope_qknorm(void* stream, void* x, long ldx, long rows, int heads, int rope_heads, const float* cos_t,
+                      const float* sin_t, long tokens_per_seq, float eps);
+
+/* Row gather dst[i] = src[idx[i]] (bf16 rows of `cols`, cols % 8 == 0): the context compaction of
+ * prepare_flash_attention_inputs (model.py:61-62) for a ragged context_attn_mask. idx: device int32 [n]. */
+int flite_gather_rows(void* stream, const void* src, void* dst, const int* idx, long n, int cols);
+
+/* TwoDimRotary tables (model.py:334-386) for an (h, w) patch grid with n_reg leading register rows. */
+int flite_rope_tables(void* stream, float* cos_t, float* sin_t, int h, int w, int n_reg, float base, int round_bf16);
+
+/* timestep_embedding (model.py:20-28) of t*1000 to bf16 [n, dim]; quantize=1 reproduces the bf16 pipeline
+ * (t -> bf16, t*1000 -> bf16; pipeline.py:260, model.py:551). */
+int flite_timestep_embedding(void* stream, const float* t, void* emb, int n, int dim, int quantize);
+
+/*
+ * Deterministic synthetic parameters (no weights are shipped): fills `out` ([numel], bf16 or
+ * fp32) with the splitmix64 counter-hash generator of oracle/weights.py keyed by (seed, name), uniform with
+ * standard deviation `std`; ones=1 fills 1.0 (norm weights). Bit-identical to the CPU generator.
+ */
+int flite_init_param(void* stream, void* out, int out_is_bf16, long numel, const char* name, unsigned long long seed,
+                     double std, int ones);
+
+/* ---------------------------------------------------------------------------------------------
+ * Model-level engine: the DiT forward (model.py:525-591 / model_v2.py:528-594) and the denoise loop
+ * (pipeline.py:250-297) as native launch sequences; weights are caller-owned device tensors bound by
+ * their state-dict names (model.py:417-479); the engine owns only its workspace.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct flite_dit_config {
+  int in_channels;            /* DiT(in_channels=...)                         */
+  int patch_size;             /* patch_size                                   */
+  int hidden_size;            /* hidden_size (num_heads * 256)                */
+  int depth;                  /* depth                                        */
+  int num_heads;              /* num_heads                                    */
+  int mlp_hidden;             /* int(hidden_size * mlp_ratio)                 */
+  int cross_attn_input_size;  /* cross_attn_input_size                        */
+  int train_bias_and_rms;     /* qkv/q/kv biases + final_norm weight          */
+  int per_block_adaln;        /* 1 = model_v2.py layout (adaLN per block, cross-attn in every block) */
+  int n_register_tokens;      /* 16 (model.py:446)                            */
+  float rope_base;            /* rope_base                                    */
+  int bf16_timestep_quant;    /* 1 = bf16 model semantics for t  */
+  int bf16_rope_tables;       /* 1 = RoPE tables rounded to bf16 (bf16 model) */
+} flite_dit_config;
+
+typedef struct flite_dit flite_dit;
+
+int flite_dit_create(const flite_dit_config* cfg, flite_dit** out);
+int flite_dit_destroy(flite_dit* dit);
+/* Bind one parameter by its state-dict key (e.g. "blocks.3.self_attn.qkv.weight"); bf16 device memory. */
+int flite_dit_bind(flite_dit* dit, const char* name, const void* ptr, long numel);
+/* Allocate the workspace for batch B (CFG included) of latents [C, h, w]; up to n_ctx context rows and
+ * n_t timestep rows. Re-entrant: a call with an equal/smaller shape is a no-op. */
+int flite_dit_prepare(flite_dit* dit, int batch, int latent_h, int latent_w, int n_ctx, int n_t);
+/* Context embeddings [cu[batch], cross_attn_input_size] bf16, packed by host cu_seqlens [batch+1]:
+ * context_proj + context_norm + per-block cross-attention K/V (step-invariant cache). */
+int flite_dit_set_context(flite_dit* dit, void* stream, const void* ctx, const int* cu_seqlens_host, int batch);
+/* Timesteps (device fp32 [n]): time embedding + adaLN/final modulation rows. quantize=1: the timesteps
+ * tensor is bf16 in the reference call, so t and t*1000 are rounded to bf16 (pipeline.py:260, model.py:551). */
+int flite_dit_set_timesteps(flite_dit* dit, void* stream, const float* t, int n, int quantize);
+/* DiT forward of latents [batch, C, h, w] (fp32 or bf16); sample b uses timestep row t_row0 + b*t_row_step.
+ * Output [batch, C, h, w] in out (bf16 if out_is_bf16 else fp32). */
+int flite_dit_forward(flite_dit* dit, void* stream, const void* x, int x_is_bf16, int batch, int t_row0,
+                      int t_row_step, void* out, int out_is_bf16);
+/*
+ * The rectified-flow denoise loop of FLitePipeline.__call__ (pipeline.py:250-297) for n_img images:
+ * per step the CFG batch [latents; latents] (uncond context first) runs through the DiT, then
+ * CFG (u + g(c-u)) or APG combine and the Euler update acc += dt*v, with acc fp32 [n_img, C, h, w]
+ * updated in place. t/dt are host arrays [n_steps]. use_graph=1 captures the loop in one hipGraph.
+ */
+int flite_dit_sample(flite_dit* dit, void* stream, float* acc, int n_img, int n_steps, const float* t_host,
+                     const float* dt_host, float guidance, int use_cfg, int apg, float apg_threshold,
+                     int use_graph);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLITE_H_ */

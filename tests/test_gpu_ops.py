@@ -1,0 +1,186 @@
+"""GPU parity of each HIP kernel (through the C ABI) against the CPU oracle / fp32 references.
+
+Tolerances (protocol P1): GEMM / attention rel-L2 <= 1e-2 vs fp32 accumulation of the same
+bf16 operands; norms/elementwise within 1-2 bf16 ulp (rel-L2 <= 8e-3); generators bit-exact.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover - these tests need the MI355X box
+    pytest.skip("no ROCm device", allow_module_level=True)
+
+from f_lite import _native as nat  # noqa: E402
+from oracle import flite_ref as R  # noqa: E402
+from oracle.weights import hash_uniform  # noqa: E402
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def test_library_loads_every_symbol():
+    lib = nat.load()
+    for name in nat.SIGNATURES:
+        assert hasattr(lib, name)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 64, 64), (256, 256, 64), (300, 200, 128), (1000, 768, 4096),
+                                   (8224, 3072, 3072)])
+def test_gemm_bias_bf16(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) * 0.05).bfloat16()
+    b = (torch.randn(N, device=DEV, generator=g) * 0.1).bfloat16()
+    ref = a.float() @ w.float().t() + b.float()
+    out = nat.gemm(a, w, b)
+    assert rel(out, ref) < 1e-2
+    out32 = nat.gemm(a, w, b, epilogue=nat.EPI_STORE_F32)
+    assert rel(out32, ref) < 1e-5
+
+
+def test_gemm_strided_operands():
+    # A with a row stride larger than K (a column slice), W slice
+    a_full = torch.randn(500, 320, device=DEV).bfloat16()
+    a = a_full[:, :256]
+    w = (torch.randn(96, 256, device=DEV) * 0.05).bfloat16()
+    out = nat.gemm(a, w, None, epilogue=nat.EPI_STORE_F32)
+    assert rel(out, a.float() @ w.float().t()) < 1e-5
+
+
+def test_gemm_swiglu():
+    M, F, K = 777, 1024, 512
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    wg = (torch.randn(F, K, device=DEV) * 0.05).bfloat16()
+    wu = (torch.randn(F, K, device=DEV) * 0.05).bfloat16()
+    ref = torch.nn.functional.silu(a.float() @ wg.float().t()) * (a.float() @ wu.float().t())
+    out = nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu)
+    assert rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_gemm_gated_residual(shared):
+    M, N, K, T = 1000, 768, 256, 300
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    nseg = (M + T - 1) // T
+    gate = torch.randn(nseg, N, device=DEV)
+    x0 = torch.randn(M, N, device=DEV)
+    y = a.float() @ w.float().t() + b.float()
+    ref = x0.clone()
+    for s in range(nseg):
+        ref[s * T:(s + 1) * T] += y[s * T:(s + 1) * T] * gate[0 if shared else s]
+    x = x0.clone()
+    nat.gemm(a, w, b, out=x, epilogue=nat.EPI_RESID_F32, gate=gate, gate_seg_stride=0 if shared else N,
+             rows_per_seg=T)
+    assert rel(x, ref) < 1e-5
+
+
+def _attn_ref(q, k, v, cu_q, cu_k, scale):
+    return R.attention_varlen(q.float().cpu(), k.float().cpu(), v.float().cpu(), cu_q.cpu(), cu_k.cpu(), scale)
+
+
+@pytest.mark.parametrize("lens_q,lens_k", [([80, 80], None), ([272, 272], None), ([4112], None),
+                                           ([100, 37], [24, 17]), ([130, 5], [512, 0]), ([64], [1])])
+def test_attention_varlen(lens_q, lens_k):
+    H, D = 2, 256
+    self_attn = lens_k is None
+    lens_k = lens_q if self_attn else lens_k
+    cu_q = torch.tensor([0] + list(torch.tensor(lens_q).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lens_k).cumsum(0)), dtype=torch.int32)
+    g = torch.Generator(device=DEV).manual_seed(sum(lens_q))
+    # unit-RMS rows like the QK-normed operands of the model (scores up to ~16)
+    q = R.own_rmsnorm(torch.randn(int(cu_q[-1]), H, D, device=DEV, generator=g), None).bfloat16()
+    k = R.own_rmsnorm(torch.randn(max(int(cu_k[-1]), 1), H, D, device=DEV, generator=g), None).bfloat16()
+    v = torch.randn(max(int(cu_k[-1]), 1), H, D, device=DEV, generator=g).bfloat16()
+    out = nat.attn_varlen(q, k, v, cu_q.to(DEV), cu_k.to(DEV), max(lens_q), D ** -0.5)
+    ref = _attn_ref(q, k, v, cu_q, cu_k, D ** -0.5)
+    assert rel(out, ref) < 1e-2
+
+
+def test_attention_spike_rescale():
+    # force the online-softmax rescale: one key far above the rest in a late tile (§5.4 rule 26)
+    H, D, L = 1, 256, 700
+    q = R.own_rmsnorm(torch.randn(L, H, D, device=DEV), None)
+    k = R.own_rmsnorm(torch.randn(L, H, D, device=DEV), None)
+    k[650] = q[3] * 1.0  # row 3's max jumps at tile 10
+    k[90] = -q[3]
+    q, k = q.bfloat16(), k.bfloat16()
+    v = torch.randn(L, H, D, device=DEV).bfloat16()
+    cu = torch.tensor([0, L], dtype=torch.int32)
+    out = nat.attn_varlen(q, k, v, cu.to(DEV), cu.to(DEV), L, 1.0)  # scale 1: scores up to 256
+    ref = _attn_ref(q, k, v, cu, cu, 1.0)
+    assert rel(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("in_bf16", [False, True])
+def test_rmsnorm_modulate(in_bf16):
+    rows, D, T = 600, 512, 250
+    x = torch.randn(rows, D, device=DEV) * 3
+    if in_bf16:
+        x = x.bfloat16()
+    w = (1 + 0.1 * torch.randn(D, device=DEV)).bfloat16()
+    nseg = (rows + T - 1) // T
+    shift = torch.randn(nseg, D, device=DEV) * 0.1
+    scale = torch.randn(nseg, D, device=DEV) * 0.1
+    out = nat.rmsnorm_modulate(x, w, shift, scale, seg_rows=T)
+    xf = x.float().cpu()
+    n = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * w.float().cpu()
+    seg = torch.arange(rows) // T
+    ref = n * (1 + scale.cpu()[seg]) + shift.cpu()[seg]
+    assert rel(out, ref) < 4e-3
+
+
+def test_rope_tables_match_reference(golden):
+    cos, sin = nat.rope_tables(12, 20, 16, 10000.0, round_bf16=False)
+    # fp32 tables: device cosf/sinf vs torch CPU within 2 ulp-ish
+    assert (cos.cpu() - golden["op.rope.cos"]).abs().max() < 2e-6
+    assert (sin.cpu() - golden["op.rope.sin"]).abs().max() < 2e-6
+    cb, sb = nat.rope_tables(12, 20, 16, 10000.0, round_bf16=True)
+    mism = (cb.cpu() != golden["op.rope_bf16.cos"]).float().mean().item()
+    assert mism < 1e-3  # bf16 rounding of 1-ulp-different fp32 values can flip a handful of entries
+
+
+def test_rope_qknorm():
+    rows, H, T = 300, 2, 150
+    x = torch.randn(rows, 3 * H * 256, device=DEV).bfloat16()
+    cos, sin = nat.rope_tables(12, 13, 16, 10000.0, round_bf16=True)
+    assert cos.shape[0] >= T
+    cos, sin = cos[:T].contiguous(), sin[:T].contiguous()
+    y = x.clone()
+    nat.rope_qknorm_(y, heads=2 * H, rope_heads=2 * H, cos=cos, sin=sin, tokens_per_seq=T)
+    xc = x.float().cpu().reshape(rows, 3, H, 256)
+    tok = torch.arange(rows) % T
+    c, s = cos.cpu()[tok][:, None, :], sin.cpu()[tok][:, None, :]
+    for part in range(2):
+        ref = R.own_rmsnorm(R.apply_rotary_emb(xc[:, part], c, s), None)
+        got = y.float().cpu().reshape(rows, 3, H, 256)[:, part]
+        assert rel(got, ref) < 4e-3
+    assert torch.equal(y[:, 2 * H * 256:], x[:, 2 * H * 256:])  # v untouched
+
+
+def test_timestep_embedding_quantized(golden):
+    t = golden["op.temb_bf16t.t"].to(DEV)
+    emb = nat.timestep_embedding(t, 512, quantize=True)
+    ref = golden["op.temb_bf16t.out"].bfloat16().float()
+    assert (emb.float().cpu() - ref).abs().max() < 8e-3  # 1 bf16 ulp at |x| <= 1
+
+
+def test_init_param_bit_exact():
+    for name, n, std in [("blocks.0.self_attn.qkv.weight", 100003, 0.02), ("register_tokens", 8192, 0.02),
+                         ("x", 5000, 1.0)]:
+        t = torch.empty(n, device=DEV, dtype=torch.float32)
+        nat.init_param_(t, name, seed=3, std=std)
+        ref = torch.from_numpy(hash_uniform(name, n, std, seed=3))
+        assert torch.equal(t.cpu(), ref)
+        tb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+        nat.init_param_(tb, name, seed=3, std=std)
+        assert torch.equal(tb.cpu(), ref.bfloat16())
