@@ -1,0 +1,267 @@
+#!/usr/bin/env python
+"""F-Lite sampling-path benchmark on MI355X (BASELINE.json metric).
+
+Metric: images/sec @1024x1024, 30 steps, F-Lite-10B bf16 (model_v2 layout), CFG 6, random-init weights and
+synthetic T5 context, including the VAE decode to uint8. One "step" of this benchmark = one image generated
+per GPU (30 CFG-batched DiT steps + VAE decode), inputs already resident in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Multi-GPU: one process per GPU, images sharded one per GPU (weak scaling); RCCL is used only to broadcast the
+shared text embedding from rank 0 before the loop (no per-step collective). Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "f-lite_amd"))
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+
+PEAK_BF16 = 256 * 4 * 1024 * 2.4e9  # 2.5166 PF/s dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM = 8.0e12
+
+
+def dit_flops(cfg: dict, H: int, W: int, steps: int, ctx_len: int = 512):
+    """Algorithmic FLOPs: per sample per step F_step, once per image F_once (context K/V +
+    context_proj); 2 FLOP per MAC, GEMM + attention, eltwise excluded."""
+    D = cfg["hidden_size"]
+    F = int(D * cfg["mlp_ratio"])
+    p = cfg["patch_size"]
+    C = cfg["in_channels"]
+    T = 16 + (H // 8 // p) * (W // 8 // p)
+    depth = cfg["depth"]
+    cross = [True if cfg["per_block_adaln"] else (i % 4 == 0 or i < 8) for i in range(depth)]
+    nc = sum(cross)
+    f_step = depth * (2 * T * D * 3 * D + 2 * T * D * D + 2 * T * D * 2 * F + 2 * T * F * D + 4 * T * T * D)
+    f_step += nc * (2 * T * D * D + 2 * T * D * D + 4 * T * ctx_len * D)
+    f_step += 2 * (T - 16) * C * p * p * D * 2
+    f_once = nc * 2 * ctx_len * D * 2 * D + 2 * ctx_len * cfg["cross_attn_input_size"] * D
+    return f_step, f_once
+
+
+def vae_flops(H: int, W: int):
+    """Flux VAE decoder conv/attention FLOPs at H x W output (2 FLOP/MAC)."""
+    from f_lite.vae import decoder_flops
+
+    return decoder_flops(H, W)
+
+
+def cpu_baseline_sample(model, cfg: dict, H: int, W: int, steps: int):
+    """Time the fp32 CPU oracle (oracle/flite_ref.py) on one DiT block at the full 1024^2 CFG batch and
+    extrapolate to a whole image (depth x steps); the VAE decode is not included in the CPU sample."""
+    from oracle import flite_ref as R
+
+    threads = torch.get_num_threads()
+    D = cfg["hidden_size"]
+    nh = cfg["num_heads"]
+    p = cfg["patch_size"]
+    hp, wp = H // 8 // p, W // 8 // p
+    T = 16 + hp * wp
+    B = 2
+    rcfg = R.DiTConfig(**{k: cfg[k] for k in ("in_channels", "patch_size", "hidden_size", "depth", "num_heads",
+                                                 "mlp_ratio", "cross_attn_input_size", "train_bias_and_rms",
+                                                 "per_block_adaln")})
+    # block 0 weights: the same bf16 tensors the GPU uses, copied to the host in fp32
+    params = {n: t.detach().float().cpu() for n, t in model.named_parameters() if n.startswith("blocks.0.")}
+    ref = R.RefDiT(rcfg, params, dtype=torch.float32)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(B * T, D, generator=g)
+    ctx = torch.randn(B * 512, D, generator=g)
+    cu = torch.tensor([0, T, 2 * T], dtype=torch.int32)
+    ccu = torch.tensor([0, 512, 1024], dtype=torch.int32)
+    mod = tuple(0.02 * torch.randn(B * T, D, generator=g) for _ in range(9))
+    cos, sin = R.rope_tables(hp, wp, D // (2 * nh), 10000.0, 16, torch.bfloat16)
+    cos, sin = cos[None].repeat(1, B, 1), sin[None].repeat(1, B, 1)
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        ref.block(0, x, cu, T, ctx, ccu, mod, cos, sin)
+        dt = time.perf_counter() - t0
+    per_image = dt * cfg["depth"] * steps
+    return {
+        "value": 1.0 / per_image,
+        "unit": "images/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"fp32 CPU oracle (oracle/flite_ref.py), 1 of {cfg['depth']} DiT blocks x 1 of {steps} steps "
+                   f"at {H}x{W} CFG batch 2 (T={T}) measured {dt:.2f} s, extrapolated x{cfg['depth'] * steps} "
+                   "per image; VAE decode excluded"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed images per GPU")
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="10b", choices=["7b", "10b"])
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--sample-steps", type=int, default=30)
+    ap.add_argument("--guidance", type=float, default=6.0)
+    ap.add_argument("--no-vae", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    from f_lite import DiT, FLitePipeline
+    from f_lite import _native as nat
+    from f_lite.model import PRESETS
+
+    cfg = dict(PRESETS[args.model])
+    model = DiT.random(seed=0, device=dev, **cfg)
+    vae = None
+    if not args.no_vae:
+        from f_lite.vae import AutoencoderKL
+
+        vae = AutoencoderKL.random(seed=0, device=dev)
+    pipe = FLitePipeline(model, vae)
+
+    # synthetic T5 context [1, 512, 4096] (uniform, std 1), generated on rank 0 and broadcast over RCCL/xGMI
+    ctx = torch.empty(1, 512, cfg["cross_attn_input_size"], device=dev, dtype=torch.bfloat16)
+    if rank == 0:
+        nat.init_param_(ctx, "synthetic.t5_context", seed=1, std=1.0)
+    if dist is not None:
+        dist.broadcast(ctx, src=0)
+
+    lh, lw = args.height // 8, args.width // 8
+
+    def latents_for(i):
+        lat = torch.empty(1, 16, lh, lw, device=dev, dtype=torch.bfloat16)
+        return nat.init_param_(lat, f"synthetic.latents.{i}", seed=2, std=1.0)
+
+    out_type = "latent" if vae is None else "uint8"
+
+    def one_image(i):
+        return pipe(prompt_embeds=ctx, latents=latents_for(i), height=args.height, width=args.width,
+                    num_inference_steps=args.sample_steps, guidance_scale=args.guidance, output_type=out_type,
+                    use_graph=not args.no_graph).images
+
+    for w in range(args.warmup):
+        one_image(rank + world * (args.steps + w))
+    kinds = {"gateup": nat.PROBE_GEMM_GATEUP, "attn": nat.PROBE_ATTN_SELF, "down": nat.PROBE_GEMM_DOWN,
+             "qkv": nat.PROBE_GEMM_QKV, "step": nat.PROBE_STEP, "none": -1}
+    eng = model.engine()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        img = one_image(rank + world * k)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # Per-launch timing of the dominant kernel: HIP event pairs on the engine stream around every launch of
+    # that kernel during one more image (the same launch sequence, run eagerly: event timestamps are not
+    # readable from a replayed hipGraph on ROCm 7.2).
+    probe_ms = []
+    if args.probe != "none":
+        eng.set_probe(kinds[args.probe], 4 * cfg["depth"] * args.sample_steps)
+        pipe(prompt_embeds=ctx, latents=latents_for(rank), height=args.height, width=args.width,
+             num_inference_steps=args.sample_steps, guidance_scale=args.guidance, output_type=out_type,
+             use_graph=False)
+        torch.cuda.synchronize()
+        probe_ms = eng.read_probe(8192)
+        eng.set_probe(-1, 0)
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed / args.steps * 1000.0
+    value = world * args.steps / elapsed
+    f_step, f_once = dit_flops(cfg, args.height, args.width, args.sample_steps)
+    f_vae = vae_flops(args.height, args.width) if vae is not None else 0.0
+    f_image = args.sample_steps * 2 * f_step + 2 * f_once + f_vae
+    D = cfg["hidden_size"]
+    F = int(D * cfg["mlp_ratio"])
+    T = 16 + (args.height // 16) * (args.width // 16)
+    M = 2 * T
+    per_launch = {
+        "gateup": (2.0 * M * 2 * F * D, "SwiGLU gate/up GEMM (M=%d, N=%d, K=%d)" % (M, 2 * F, D)),
+        "down": (2.0 * M * D * F, "down GEMM + gated residual (M=%d, N=%d, K=%d)" % (M, D, F)),
+        "qkv": (2.0 * M * 3 * D * D, "qkv GEMM (M=%d, N=%d, K=%d)" % (M, 3 * D, D)),
+        "attn": (2 * 4.0 * T * T * D, "self-attention (B=2, H=%d, T=%d, hd=256)" % (cfg["num_heads"], T)),
+        "step": (2.0 * f_step, "one CFG-batched denoise step"),
+    }
+    roofline = None
+    if probe_ms:
+        avg_ms = sum(probe_ms) / len(probe_ms)
+        flops, what = per_launch[args.probe]
+        achieved = flops / (avg_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(PEAK_BF16 / 1e12, 1),
+                    "unit": "TFLOP/s", "frac": round(achieved * 1e12 / PEAK_BF16, 4), "traffic": None,
+                    "kernel": what, "launches": len(probe_ms), "avg_ms": round(avg_ms, 4),
+                    "algorithmic_flops_per_launch": flops}
+        pmc = ROOT / "profiles" / "pmc_traffic.json"
+        if pmc.exists():
+            try:
+                tr = json.loads(pmc.read_text()).get(args.probe)
+                if tr:
+                    roofline["traffic"] = tr["hbm_bytes_per_launch"]
+            except Exception:
+                pass
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline_sample(model, cfg, args.height, args.width, args.sample_steps)
+
+    line = {
+        "metric": "images/sec @%dx%d, %d steps, F-Lite-%s bf16" % (args.height, args.width, args.sample_steps,
+                                                                   args.model.upper()),
+        "value": round(value, 5),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (random-init weights from the deterministic generator; synthetic T5 context "
+                "[1,512,4096]; seeded latents)",
+        "config": {"workload": "F-Lite-%s %s, %dx%d, %d steps, CFG %.1f, %s" % (
+            args.model.upper(), "model_v2 layout" if cfg["per_block_adaln"] else "model.py layout",
+            args.width, args.height, args.sample_steps, args.guidance,
+            "VAE decode to uint8" if vae is not None else "latents only (no VAE)"),
+                   "images_per_gpu_per_step": 1, "cfg_batch": 2, "parallelism": "replica dp%d" % world,
+                   "hipgraph": not args.no_graph},
+        "mfma_util_image": round(f_image * value / world / PEAK_BF16, 4),
+        "algorithmic_flops_per_image": f_image,
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -200,3 +200,52 @@ int flite_init_param(void* stream, void* out, int out_is_bf16, long numel, const
   return hash_init(out, out_is_bf16, numel, name, seed, std, (hipStream_t)stream);
 }
 }  // extern "C"
+
+extern "C" {
+int flite_dit_set_probe(flite_dit* dit, int kind, int max_pairs) {
+  FLITE_REQUIRE(dit, "flite_dit_set_probe: null engine");
+  return dit->eng->set_probe(kind, max_pairs);
+}
+int flite_dit_read_probe(flite_dit* dit, float* ms, int cap, int* n) {
+  FLITE_REQUIRE(dit && ms && n, "flite_dit_read_probe: null argument");
+  return dit->eng->read_probe(ms, cap, n);
+}
+}  // extern "C"
+
+extern "C" {
+int flite_conv3x3_pack_weight(void* stream, const void* w, void* packed, int cout, int cin, int cin_pad) {
+  FLITE_REQUIRE(w && packed && cin_pad % 64 == 0 && cin_pad >= cin, "flite_conv3x3_pack_weight: bad arguments");
+  return pack_conv_weight((const bf16_t*)w, (bf16_t*)packed, cout, cin, cin_pad, (hipStream_t)stream);
+}
+
+int flite_conv3x3_bf16(void* stream, const void* x, int batch, int h, int w, int cin, int upsample,
+                       const void* w_packed, const void* bias, int cout, void* out, const void* resid,
+                       int out_is_f32) {
+  FLITE_REQUIRE(batch == 1, "flite_conv3x3_bf16: one image per call");
+  GemmParams g;
+  g.conv_in = (const bf16_t*)x;
+  g.conv_c = cin;
+  g.conv_ih = h;
+  g.conv_iw = w;
+  g.conv_up = upsample ? 1 : 0;
+  g.conv_oh = upsample ? 2 * h : h;
+  g.conv_ow = upsample ? 2 * w : w;
+  g.conv_in_bytes = (long)h * w * cin * 2;
+  g.W = (const bf16_t*)w_packed;
+  g.ldw = 9L * cin;
+  g.bias = (const bf16_t*)bias;
+  g.out = out;
+  g.ldo = cout;
+  g.resid = (const bf16_t*)resid;
+  g.M = g.conv_oh * g.conv_ow;
+  g.N = cout;
+  g.K = 9 * cin;
+  return gemm_bf16(g, out_is_f32 ? EPI_STORE_F32 : EPI_STORE_BF16, (hipStream_t)stream);
+}
+
+int flite_group_norm(void* stream, const void* x, void* y, long rows, int channels, int groups, const void* gamma,
+                     const void* beta, float eps, int silu, double* stats_workspace) {
+  return group_norm((const bf16_t*)x, (bf16_t*)y, rows, channels, groups, (const bf16_t*)gamma,
+                    (const bf16_t*)beta, eps, silu != 0, stats_workspace, (hipStream_t)stream);
+}
+}  // extern "C"

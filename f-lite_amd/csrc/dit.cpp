@@ -382,7 +382,9 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.M = (int)M_;
     g.N = 3 * D;
     g.K = D;
+    if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
     if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+    if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
   }
   {
     RopeNormParams rn;
@@ -412,7 +414,9 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.head_dim = HEAD_DIM;
     a.max_q = T_;
     a.scale = 1.0f / sqrtf((float)HEAD_DIM);
+    if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
     if (attn_fwd(a, s)) return 1;
+    if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
   }
   if (resid(obuf_, D, b.proj_w, D, gate_sa)) return 1;
 
@@ -472,9 +476,52 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.M = (int)M_;
     g.N = 2 * F;
     g.K = D;
+    if (probe_begin(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
     if (gemm_bf16(g, EPI_SWIGLU_BF16, s)) return 1;
+    if (probe_end(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
   }
+  if (probe_begin(s, FLITE_PROBE_GEMM_DOWN)) return 1;
   if (resid(hbuf_, F, b.down_w, F, gate_mlp)) return 1;
+  if (probe_end(s, FLITE_PROBE_GEMM_DOWN)) return 1;
+  return 0;
+}
+
+int DitEngine::set_probe(int kind, int max_pairs) {
+  for (hipEvent_t e : probe_ev_) hipEventDestroy(e);
+  probe_ev_.clear();
+  probe_n_ = 0;
+  probe_kind_ = kind;
+  if (gexec_) {  // a cached graph holds (or lacks) the old probe nodes
+    hipGraphExecDestroy(gexec_);
+    gexec_ = nullptr;
+  }
+  if (kind < 0) return 0;
+  FLITE_REQUIRE(max_pairs > 0 && max_pairs <= 100000, "set_probe: bad max_pairs");
+  probe_ev_.resize(2 * (size_t)max_pairs);
+  for (auto& e : probe_ev_) FLITE_HIP_CHECK(hipEventCreate(&e));
+  return 0;
+}
+
+int DitEngine::probe_begin(hipStream_t s, int kind) {
+  if (kind != probe_kind_ || probe_n_ * 2 + 1 >= (int)probe_ev_.size()) return 0;
+  FLITE_HIP_CHECK(hipEventRecord(probe_ev_[2 * probe_n_], s));
+  return 0;
+}
+
+int DitEngine::probe_end(hipStream_t s, int kind) {
+  if (kind != probe_kind_ || probe_n_ * 2 + 1 >= (int)probe_ev_.size()) return 0;
+  FLITE_HIP_CHECK(hipEventRecord(probe_ev_[2 * probe_n_ + 1], s));
+  ++probe_n_;
+  return 0;
+}
+
+int DitEngine::read_probe(float* ms, int cap, int* n) {
+  *n = 0;
+  for (int i = 0; i < probe_n_ && i < cap; ++i) {
+    FLITE_HIP_CHECK(hipEventSynchronize(probe_ev_[2 * i + 1]));
+    FLITE_HIP_CHECK(hipEventElapsedTime(&ms[i], probe_ev_[2 * i], probe_ev_[2 * i + 1]));
+    *n = i + 1;
+  }
   return 0;
 }
 
@@ -557,8 +604,11 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
   if (set_timesteps(s, tdev_, n_steps, cfg.bf16_timestep_quant)) return 1;
 
   auto body = [&](hipStream_t st) -> int {
+    probe_n_ = 0;
     for (int i = 0; i < n_steps; ++i) {
+      if (probe_begin(st, FLITE_PROBE_STEP)) return 1;
       if (forward(st, acc, false, Bi, dup, i, 0)) return 1;
+      if (probe_end(st, FLITE_PROBE_STEP)) return 1;
       if (apg) {
         if (apg_euler(fout_, acc, Bi, C, Hl_, Wl_, P, guidance, apg_thr, dt_host[i], st)) return 1;
       } else {

@@ -49,7 +49,18 @@ class DitEngine {
   const flite_dit_config cfg;
   int D, H, F, R, P, C;
 
+  // launch probe: HIP event pairs around every launch of one kernel class (FLITE_PROBE_*), on the stream
+  // the kernel is launched on (also inside a captured graph, as event-record nodes)
+  int set_probe(int kind, int max_pairs);
+  int read_probe(float* ms, int cap, int* n);
+
  private:
+  int probe_begin(hipStream_t s, int kind);
+  int probe_end(hipStream_t s, int kind);
+  int probe_kind_ = -1;
+  std::vector<hipEvent_t> probe_ev_;
+  int probe_n_ = 0;
+
   int run_block(hipStream_t s, int blk, const float* mod, long mseg);
   int alloc(void** p, size_t bytes);
   void free_ws();

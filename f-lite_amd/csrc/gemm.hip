@@ -31,7 +31,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
   __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)ldst, 16, 0, 0);
 }
 
-template <int EPI>
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, void* ldst) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)ldst, 16, voff, 0, 0, 0);
+}
+
+// CONV = implicit-GEMM 3x3 convolution (pad 1) over an NHWC bf16 input: A row m = output pixel, k = (tap, c)
+// with tap = ky*3+kx. Each 64-wide k-tile is one tap and 64 consecutive channels (128 contiguous bytes of
+// one input pixel) -> staged by buffer_load ... lds, whose range check returns 0 for the padding pixels.
+// `upsample` folds nearest-2x interpolation into the addressing (Upsample2D + conv).
+template <int EPI, bool CONV>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -65,13 +73,27 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
   // glds instruction q (0..31) covers tile rows 8q..8q+7; lane -> row 8q + lane/8, 16-B chunk (lane&7)^swz.
   const bf16_t* a_src[4];
   const bf16_t* w_src[4];
+  int cy[4], cx[4];
+  unsigned cbase[4];  // element offset of (batch, chunk) for CONV
+  __amdgpu_buffer_rsrc_t crs;
+  if constexpr (CONV) crs = __builtin_amdgcn_make_buffer_rsrc((void*)p.conv_in, 0, (int)p.conv_in_bytes, 0x00020000);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int q = wave * 4 + i;
     const int row = q * 8 + (lane >> 3);
     const int chunk = (lane & 7) ^ swz(row);
     const int am = min(m0 + row, p.M - 1);
-    a_src[i] = p.A + (long)am * p.lda + chunk * 8;
+    if constexpr (CONV) {
+      const int hw = p.conv_oh * p.conv_ow;
+      const int b = am / hw;
+      const int r = am - b * hw;
+      cy[i] = r / p.conv_ow;
+      cx[i] = r - cy[i] * p.conv_ow;
+      cbase[i] = (unsigned)((long)b * p.conv_ih * p.conv_iw * p.conv_c + chunk * 8);
+      a_src[i] = nullptr;
+    } else {
+      a_src[i] = p.A + (long)am * p.lda + chunk * 8;
+    }
     const int wn = min(n0 + row, p.N - 1);
     const bf16_t* wbase;
     long wrow;
@@ -90,10 +112,30 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
   auto stage = [&](int kt, int buf) {
     char* base = smem + buf * STAGE_BYTES;
     const int koff = kt * BK;
+    if constexpr (CONV) {
+      const int tap = koff / p.conv_c;
+      const int c0 = koff - tap * p.conv_c;
+      const int ky = tap / 3 - 1, kx = tap % 3 - 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = wave * 4 + i;
+        const int iy = cy[i] + ky, ix = cx[i] + kx;
+        const bool ok = iy >= 0 && iy < p.conv_oh && ix >= 0 && ix < p.conv_ow;
+        const int sy = p.conv_up ? (iy >> 1) : iy;
+        const int sx = p.conv_up ? (ix >> 1) : ix;
+        const unsigned e = cbase[i] + (unsigned)((sy * p.conv_iw + sx) * p.conv_c + c0);
+        blds16(crs, ok ? e * 2u : 0x80000000u, base + q * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = wave * 4 + i;
+        glds16(a_src[i] + koff, base + q * 1024);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = wave * 4 + i;
-      glds16(a_src[i] + koff, base + q * 1024);
       glds16(w_src[i] + koff, base + TILE_BYTES + q * 1024);
     }
   };
@@ -199,6 +241,12 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
         }
         if constexpr (EPI == EPI_STORE_BF16) {
           bf16_t* o = (bf16_t*)p.out + om * p.ldo + n;
+          if (p.resid != nullptr) {  // ResnetBlock2D / attention residual (x + h), same layout as out
+            const bf16_t* rr = p.resid + om * p.ldo + n;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) v[r] += bf2f(rr[r]);
+          }
           if (n + 3 < p.N) {
             u32x2 w;
             w.x = pack2bf(v[0], v[1]);
@@ -237,24 +285,32 @@ int launch(const GemmParams& p, hipStream_t s) {
   const int num_m = (p.M + BM - 1) / BM;
   const int num_n = (p.N + BN - 1) / BN;
   const int grid = num_m * num_n;
-  hipLaunchKernelGGL(gemm_bf16_kernel<EPI>, dim3(grid), dim3(NT), LDS_BYTES, s, p);
+  if (p.conv_in != nullptr)
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true>), dim3(grid), dim3(NT), LDS_BYTES, s, p);
+  else
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false>), dim3(grid), dim3(NT), LDS_BYTES, s, p);
   return 0;
 }
 
 bool attrs_done = false;
 
+template <int EPI>
+hipError_t set_attrs() {
+  hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             LDS_BYTES);
+}
+
 }  // namespace
 
 int gemm_init() {
   if (attrs_done) return 0;
-  FLITE_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI_STORE_BF16>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-  FLITE_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI_STORE_F32>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-  FLITE_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI_RESID_F32>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-  FLITE_HIP_CHECK(hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI_SWIGLU_BF16>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+  FLITE_HIP_CHECK(set_attrs<EPI_STORE_BF16>());
+  FLITE_HIP_CHECK(set_attrs<EPI_STORE_F32>());
+  FLITE_HIP_CHECK(set_attrs<EPI_RESID_F32>());
+  FLITE_HIP_CHECK(set_attrs<EPI_SWIGLU_BF16>());
   attrs_done = true;
   return 0;
 }
@@ -262,16 +318,27 @@ int gemm_init() {
 int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
   FLITE_REQUIRE(p.M > 0 && p.N > 0 && p.K > 0, "gemm: empty problem");
   FLITE_REQUIRE(p.K % BK == 0, "gemm: K must be a multiple of 64");
-  FLITE_REQUIRE(p.lda % 8 == 0 && p.ldw % 8 == 0, "gemm: lda/ldw must be multiples of 8 elements");
-  FLITE_REQUIRE(((uintptr_t)p.A & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "gemm: A/W must be 16-B aligned");
+  FLITE_REQUIRE(p.ldw % 8 == 0, "gemm: ldw must be a multiple of 8 elements");
+  FLITE_REQUIRE(((uintptr_t)p.W & 15) == 0, "gemm: W must be 16-B aligned");
+  if (p.conv_in != nullptr) {
+    FLITE_REQUIRE(p.conv_c % 64 == 0, "conv: input channels must be a multiple of 64");
+    FLITE_REQUIRE(p.K == 9 * p.conv_c, "conv: K must be 9 * C_in");
+    FLITE_REQUIRE(p.conv_oh == (p.conv_up ? 2 : 1) * p.conv_ih && p.conv_ow == (p.conv_up ? 2 : 1) * p.conv_iw,
+                  "conv: output size must equal input size (x2 with upsample)");
+    FLITE_REQUIRE(p.conv_in_bytes < (1L << 31), "conv: input must be < 2 GiB (32-bit buffer offsets)");
+    FLITE_REQUIRE(epi == EPI_STORE_BF16 || epi == EPI_STORE_F32, "conv: store epilogues only");
+  } else {
+    FLITE_REQUIRE(p.lda % 8 == 0, "gemm: lda must be a multiple of 8 elements");
+    FLITE_REQUIRE(((uintptr_t)p.A & 15) == 0, "gemm: A must be 16-B aligned");
+  }
   if (gemm_init()) return 1;
   switch (epi) {
     case EPI_STORE_BF16:
-      FLITE_REQUIRE(p.ldo % 4 == 0, "gemm: ldo must be a multiple of 4");
+      FLITE_REQUIRE(p.ldo % 4 == 0 || p.N < 4, "gemm: ldo must be a multiple of 4 (or N < 4)");
       launch<EPI_STORE_BF16>(p, stream);
       break;
     case EPI_STORE_F32:
-      FLITE_REQUIRE(p.ldo % 4 == 0, "gemm: ldo must be a multiple of 4");
+      FLITE_REQUIRE(p.ldo % 4 == 0 || p.N < 4, "gemm: ldo must be a multiple of 4 (or N < 4)");
       launch<EPI_STORE_F32>(p, stream);
       break;
     case EPI_RESID_F32:

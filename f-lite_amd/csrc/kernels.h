@@ -27,6 +27,12 @@ struct GemmParams {
   int act = 0;                   // 1: SiLU after bias (time_embed / adaLN inputs, model.py:448-456)
   // output row mapping: out_row = (m / out_seg) * out_seg_stride + out_seg_off + m % out_seg (0 = identity)
   long out_seg = 0, out_seg_stride = 0, out_seg_off = 0;
+  const bf16_t* resid = nullptr;  // STORE_BF16: residual added before the store (same layout as out)
+  // implicit-GEMM 3x3 conv (pad 1): A is read from the NHWC input instead of p.A; M = B*oh*ow, K = 9*C,
+  // W = packed weight [Cout][ky][kx][C]; conv_up = nearest-2x upsample folded in (oh = 2*ih)
+  const bf16_t* conv_in = nullptr;
+  long conv_in_bytes = 0;
+  int conv_ih = 0, conv_iw = 0, conv_c = 0, conv_oh = 0, conv_ow = 0, conv_up = 0;
 };
 
 int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream);
@@ -107,4 +113,15 @@ namespace flite {
 uint64_t fnv1a64(const char* s);
 int hash_init(void* out, int out_bf16, long n, const char* name, uint64_t seed, double std, hipStream_t s);
 int fill_bf16(bf16_t* out, long n, float v, hipStream_t s);
+}  // namespace flite
+
+namespace flite {
+// VAE decoder helpers (vae.hip)
+int group_norm(const bf16_t* x, bf16_t* y, long rows, int C, int G, const bf16_t* gamma, const bf16_t* beta,
+               float eps, bool silu, double* stats, hipStream_t s);
+int softmax_rows(const float* S, bf16_t* P, int R, int L, float scale, hipStream_t s);
+int transpose_bf16(const bf16_t* x, bf16_t* y, int R, int C, hipStream_t s);
+int latent_to_nhwc(const float* z, bf16_t* x, int C, int Cpad, int hw, float scaling, float shift, hipStream_t s);
+int to_uint8(const float* o, int ld, unsigned char* img, long hw, hipStream_t s);
+int pack_conv_weight(const bf16_t* w, bf16_t* o, int Cout, int Cin, int Cpad, hipStream_t s);
 }  // namespace flite

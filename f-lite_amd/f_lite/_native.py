@@ -68,7 +68,23 @@ SIGNATURES = {
     "flite_dit_set_timesteps": (_i, [_vp, _vp, _vp, _i, _i]),
     "flite_dit_forward": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _i]),
     "flite_dit_sample": (_i, [_vp, _vp, _vp, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _f, _i, _i, _f, _i]),
+    "flite_conv3x3_pack_weight": (_i, [_vp, _vp, _vp, _i, _i, _i]),
+    "flite_conv3x3_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i]),
+    "flite_group_norm": (_i, [_vp, _vp, _vp, _l, _i, _i, _vp, _vp, _f, _i, _vp]),
+    "flite_vae_create": (_i, [_vp, ctypes.POINTER(_vp)]),
+    "flite_vae_destroy": (_i, [_vp]),
+    "flite_vae_bind": (_i, [_vp, _cp, _vp, _l]),
+    "flite_vae_prepare": (_i, [_vp, _i, _i]),
+    "flite_vae_decode_uint8": (_i, [_vp, _vp, _vp, _i, _vp, _f, _f]),
+    "flite_dit_set_probe": (_i, [_vp, _i, _i]),
+    "flite_dit_read_probe": (_i, [_vp, ctypes.POINTER(_f), _i, ctypes.POINTER(_i)]),
 }
+
+PROBE_GEMM_GATEUP = 0
+PROBE_ATTN_SELF = 1
+PROBE_GEMM_DOWN = 2
+PROBE_GEMM_QKV = 3
+PROBE_STEP = 4
 
 
 class FliteError(RuntimeError):
@@ -284,6 +300,15 @@ class DitEngine:
                                          int(out.dtype == torch.bfloat16)), "flite_dit_forward")
         return out
 
+    def set_probe(self, kind: int, max_pairs: int = 4096):
+        check(self.lib.flite_dit_set_probe(self.h, kind, max_pairs), "flite_dit_set_probe")
+
+    def read_probe(self, cap: int = 4096):
+        buf = (_f * cap)()
+        n = _i(0)
+        check(self.lib.flite_dit_read_probe(self.h, buf, cap, ctypes.byref(n)), "flite_dit_read_probe")
+        return list(buf[: n.value])
+
     def sample(self, acc: torch.Tensor, n_img, t_list, dt_list, guidance, use_cfg, apg=False, apg_thr=0.03,
                use_graph=True):
         require_gpu(acc, "latents", torch.float32)
@@ -294,3 +319,86 @@ class DitEngine:
                                         float(guidance), int(use_cfg), int(apg), float(apg_thr), int(use_graph)),
               "flite_dit_sample")
         return acc
+
+
+class VaeConfig(ctypes.Structure):
+    """flite_vae_config (include/flite.h)."""
+
+    _fields_ = [
+        ("latent_channels", _i),
+        ("n_blocks", _i),
+        ("block_out_channels", _i * 4),
+        ("layers_per_block", _i),
+        ("norm_groups", _i),
+        ("mid_attention", _i),
+    ]
+
+
+class VaeEngine:
+    """Owner of a native flite_vae handle (the Flux VAE decoder + uint8 post-processing)."""
+
+    def __init__(self, config):
+        self.lib = load()
+        c = VaeConfig()
+        c.latent_channels = config.latent_channels
+        boc = list(config.block_out_channels)
+        c.n_blocks = len(boc)
+        if len(boc) != 4:
+            raise FliteError("VAE: 4 decoder blocks expected")
+        for i, v in enumerate(boc):
+            c.block_out_channels[i] = v
+        c.layers_per_block = config.layers_per_block
+        c.norm_groups = config.norm_num_groups
+        c.mid_attention = int(bool(config.mid_block_add_attention))
+        self.h = _vp()
+        check(self.lib.flite_vae_create(ctypes.byref(c), ctypes.byref(self.h)), "flite_vae_create")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.flite_vae_destroy(self.h)
+        except Exception:
+            pass
+
+    def bind(self, name, t):
+        require_gpu(t, name, torch.bfloat16)
+        check(self.lib.flite_vae_bind(self.h, name.encode(), t.data_ptr(), t.numel()), f"vae bind({name})")
+
+    def prepare(self, h, w):
+        check(self.lib.flite_vae_prepare(self.h, h, w), "flite_vae_prepare")
+
+    def decode_uint8(self, z, img, scaling, shift):
+        require_gpu(z, "latents", torch.float32)
+        require_gpu(img, "images", torch.uint8)
+        check(self.lib.flite_vae_decode_uint8(self.h, stream_ptr(z.device), z.data_ptr(), z.shape[0], img.data_ptr(),
+                                              float(scaling), float(shift)), "flite_vae_decode_uint8")
+        return img
+
+
+def conv3x3(x_nhwc, weight, bias=None, upsample=False, resid=None, out_f32=False):
+    """nn.Conv2d(k=3, pad=1) (+ nearest-2x upsample first) on NHWC bf16 [h, w, cin]; weight [cout, cin, 3, 3]."""
+    lib = load()
+    h, w, cin = x_nhwc.shape
+    cout = weight.shape[0]
+    cpad = (weight.shape[1] + 63) // 64 * 64
+    if cin != cpad:
+        raise FliteError("conv3x3: input channels must be zero-padded to a multiple of 64")
+    packed = torch.empty(cout, 9, cpad, device=x_nhwc.device, dtype=torch.bfloat16)
+    s = stream_ptr(x_nhwc.device)
+    check(lib.flite_conv3x3_pack_weight(s, weight.data_ptr(), packed.data_ptr(), cout, weight.shape[1], cpad),
+          "flite_conv3x3_pack_weight")
+    H, W = (2 * h, 2 * w) if upsample else (h, w)
+    out = torch.empty(H, W, cout, device=x_nhwc.device, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    check(lib.flite_conv3x3_bf16(s, x_nhwc.data_ptr(), 1, h, w, cin, int(upsample), packed.data_ptr(), _ptr(bias),
+                                 cout, out.data_ptr(), _ptr(resid), int(out_f32)), "flite_conv3x3_bf16")
+    return out
+
+
+def group_norm(x, groups, gamma, beta, eps=1e-6, silu=False):
+    lib = load()
+    rows, C = x.shape
+    y = torch.empty_like(x)
+    stats = torch.empty(2 * groups, device=x.device, dtype=torch.float64)
+    check(lib.flite_group_norm(stream_ptr(x.device), x.data_ptr(), y.data_ptr(), rows, C, groups, gamma.data_ptr(),
+                               beta.data_ptr(), eps, int(silu), stats.data_ptr()), "flite_group_norm")
+    return y

@@ -142,6 +142,58 @@ int flite_dit_sample(flite_dit* dit, void* stream, float* acc, int n_img, int n_
                      const float* dt_host, float guidance, int use_cfg, int apg, float apg_threshold,
                      int use_graph);
 
+/*
+ * 3x3 convolution, padding 1, stride 1 (nn.Conv2d of the diffusers VAE decoder), optionally preceded by a
+ * nearest-2x upsample (Upsample2D), as an implicit-GEMM on MFMA. x: NHWC bf16 [h, w, cin] (one image,
+ * cin % 64 == 0); w_packed from flite_conv3x3_pack_weight ([cout][3][3][cin_pad], cin zero-padded to a
+ * multiple of 64); out NHWC [H, W, cout] bf16 (or fp32); resid (optional, bf16, out layout) is added.
+ */
+int flite_conv3x3_pack_weight(void* stream, const void* w, void* packed, int cout, int cin, int cin_pad);
+int flite_conv3x3_bf16(void* stream, const void* x, int batch, int h, int w, int cin, int upsample,
+                       const void* w_packed, const void* bias, int cout, void* out, const void* resid,
+                       int out_is_f32);
+/* GroupNorm (+SiLU) over NHWC bf16 rows (torch.nn.GroupNorm semantics); stats_workspace: device double[2*groups]. */
+int flite_group_norm(void* stream, const void* x, void* y, long rows, int channels, int groups, const void* gamma,
+                     const void* beta, float eps, int silu, double* stats_workspace);
+
+/* ---------------------------------------------------------------------------------------------
+ * VAE decoder engine: diffusers AutoencoderKL.decode (FLUX.1 VAE config) as called at pipeline.py:301-307,
+ * plus the uint8 post-processing of pipeline.py:324-326. Parameters bound by their diffusers state-dict keys
+ * ("decoder.conv_in.weight", "decoder.up_blocks.2.resnets.0.conv_shortcut.weight", ...).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct flite_vae_config {
+  int latent_channels;        /* 16 */
+  int n_blocks;               /* len(block_out_channels) = 4 */
+  int block_out_channels[4];  /* (128, 256, 512, 512) */
+  int layers_per_block;       /* 2 (decoder uses layers_per_block + 1 resnets per up block) */
+  int norm_groups;            /* 32 */
+  int mid_attention;          /* 1 */
+} flite_vae_config;
+
+typedef struct flite_vae flite_vae;
+
+int flite_vae_create(const flite_vae_config* cfg, flite_vae** out);
+int flite_vae_destroy(flite_vae* vae);
+int flite_vae_bind(flite_vae* vae, const char* name, const void* ptr, long numel);
+/* Workspace + packed conv weights for latents of [latent_channels, latent_h, latent_w]. */
+int flite_vae_prepare(flite_vae* vae, int latent_h, int latent_w);
+/* latents fp32 [n_img, C, h, w] -> images uint8 [n_img, 8h, 8w, 3] (device), decoding z/scaling + shift. */
+int flite_vae_decode_uint8(flite_vae* vae, void* stream, const float* latents, int n_img, void* images,
+                           float scaling_factor, float shift_factor);
+
+/*
+ * Launch probe (measurement): bracket every launch of one kernel class with a pair of HIP events on the
+ * stream it is launched on (inside the captured loop too). read returns the per-launch milliseconds of the
+ * latest run (pairs in launch order). kind < 0 disables.
+ */
+#define FLITE_PROBE_GEMM_GATEUP 0 /* SwiGLU gate/up GEMM (largest kernel, ~38% of FLOPs) */
+#define FLITE_PROBE_ATTN_SELF 1   /* self-attention flash kernel */
+#define FLITE_PROBE_GEMM_DOWN 2   /* MLP down-projection GEMM + gated residual */
+#define FLITE_PROBE_GEMM_QKV 3    /* qkv projection GEMM */
+#define FLITE_PROBE_STEP 4        /* one whole denoise step (DiT forward + CFG/Euler) */
+int flite_dit_set_probe(flite_dit* dit, int kind, int max_pairs);
+int flite_dit_read_probe(flite_dit* dit, float* ms, int cap, int* n);
+
 #ifdef __cplusplus
 }
 #endif
