@@ -127,6 +127,7 @@ def main():
 
     from f_lite import DiT, FLitePipeline
     from f_lite import _native as nat
+    from f_lite.distributed import broadcast_context, image_indices, max_over_ranks
     from f_lite.model import PRESETS
 
     cfg = dict(PRESETS[args.model])
@@ -142,8 +143,7 @@ def main():
     ctx = torch.empty(1, 512, cfg["cross_attn_input_size"], device=dev, dtype=torch.bfloat16)
     if rank == 0:
         nat.init_param_(ctx, "synthetic.t5_context", seed=1, std=1.0)
-    if dist is not None:
-        dist.broadcast(ctx, src=0)
+    broadcast_context(ctx, src=0)
 
     lh, lw = args.height // 8, args.width // 8
 
@@ -158,8 +158,9 @@ def main():
                     num_inference_steps=args.sample_steps, guidance_scale=args.guidance, output_type=out_type,
                     use_graph=not args.no_graph).images
 
+    mine = image_indices(world * (args.steps + args.warmup), rank, world)  # image i -> GPU i mod N
     for w in range(args.warmup):
-        one_image(rank + world * (args.steps + w))
+        one_image(mine[args.steps + w])
     kinds = {"gateup": nat.PROBE_GEMM_GATEUP, "attn": nat.PROBE_ATTN_SELF, "down": nat.PROBE_GEMM_DOWN,
              "qkv": nat.PROBE_GEMM_QKV, "step": nat.PROBE_STEP, "none": -1}
     eng = model.engine()
@@ -169,7 +170,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        img = one_image(rank + world * k)
+        img = one_image(mine[k])
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -187,10 +188,7 @@ def main():
         torch.cuda.synchronize()
         probe_ms = eng.read_probe(8192)
         eng.set_probe(-1, 0)
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = max_over_ranks(elapsed, device=dev)
     if rank != 0:
         dist.destroy_process_group()
         return

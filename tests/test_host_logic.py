@@ -1,0 +1,106 @@
+"""CPU: host-side logic of the drop-in boundary (no kernels): parameter inventory, config, schedule,
+FLOP accounting, fail-loudly behaviour."""
+import json
+import math
+
+import pytest
+import torch
+
+from f_lite import APGConfig, DiT, FLitePipeline, FLitePipelineOutput
+from f_lite._native import FliteError
+from f_lite.model import PRESETS
+from f_lite.pipeline import flow_schedule
+from oracle import flite_ref as R
+from oracle.vae_ref import vae_param_shapes
+from oracle.weights import param_shapes
+
+
+def test_public_names():
+    import f_lite
+
+    assert set(f_lite.__all__) == {"FLitePipeline", "FLitePipelineOutput", "APGConfig", "DiT"}
+    assert APGConfig().enabled is True and APGConfig().orthogonal_threshold == 0.03
+
+
+@pytest.mark.parametrize("name", ["7b", "10b", "tiny", "tiny_v2"])
+def test_state_dict_inventory_matches_reference(name):
+    with torch.device("meta"):
+        m = DiT(**PRESETS[name])
+    sd = m.state_dict()
+    ref = param_shapes(dict(PRESETS[name]))
+    assert set(sd) == set(ref)
+    assert all(tuple(sd[k].shape) == tuple(ref[k]) for k in ref)
+
+
+def test_reference_ctor_defaults():
+    with torch.device("meta"):
+        m = DiT()
+    c = m.config
+    assert (c.in_channels, c.patch_size, c.hidden_size, c.depth, c.num_heads, c.mlp_ratio, c.cross_attn_input_size) \
+        == (4, 2, 1152, 28, 16, 4.0, 128)
+    # reference zero-init of the adaLN / final layers (model.py:455-456,476-479)
+    assert m.adaLN_modulation[1].weight.is_meta
+
+
+def test_v2_module_alias():
+    from f_lite.model_v2 import DiT as DiT2
+
+    with torch.device("meta"):
+        m = DiT2(**{k: v for k, v in PRESETS["tiny"].items() if k != "per_block_adaln"})
+    assert m.per_block_adaln and all(b.cross_attn is not None for b in m.blocks)
+
+
+def test_schedule_matches_reference(golden_meta):
+    for key, rows in golden_meta["schedule"].items():
+        hw, n = key.split(".")
+        h, w = map(int, hw.split("x"))
+        got = flow_schedule(int(n), h // 8, w // 8)
+        assert [(t, dt) for t, dt in got] == [tuple(r) for r in rows]
+
+
+def test_forward_on_cpu_raises():
+    m = DiT(**PRESETS["tiny"])
+    with pytest.raises(FliteError):
+        m(torch.zeros(1, 16, 8, 8), torch.zeros(1, 4, 128), torch.tensor([0.5]))
+    with pytest.raises(TypeError):
+        m(torch.zeros(1, 16, 8, 8), torch.zeros(1, 4, 128))
+
+
+def test_pipeline_requires_embeddings_without_text_encoder():
+    m = DiT(**PRESETS["tiny"])
+    p = FLitePipeline(m)
+    with pytest.raises(ValueError):
+        p.encode_prompt("a cat")
+
+
+def test_save_and_load_config_roundtrip(tmp_path):
+    m = DiT(**PRESETS["tiny"])
+    m.save_pretrained(tmp_path / "dit_model")
+    cfg = json.loads((tmp_path / "dit_model" / "config.json").read_text())
+    assert cfg["hidden_size"] == 512 and cfg["_class_name"] == "DiT"
+    m2 = DiT.from_pretrained(tmp_path, subfolder="dit_model", torch_dtype=torch.float32, device="cpu")
+    for (k, a), (k2, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert k == k2 and torch.equal(a, b)
+
+
+def test_vae_inventory():
+    from f_lite.vae import AutoencoderKL
+
+    with torch.device("meta"):
+        v = AutoencoderKL()
+    sd = v.state_dict()
+    ref = vae_param_shapes()
+    assert set(sd) == set(ref) and all(tuple(sd[k].shape) == ref[k] for k in ref)
+    assert sum(math.prod(s) for s in ref.values()) == 49545475
+
+
+def test_flop_accounting_matches_survey():
+    import bench
+
+    f_step, f_once = bench.dit_flops(PRESETS["10b"], 1024, 1024, 30)
+    assert abs(f_step / 1e12 - 65.23) < 0.01 and abs(f_once / 1e9 - 786.0) < 0.1
+    f_step7, f_once7 = bench.dit_flops(PRESETS["7b"], 1024, 1024, 30)
+    assert abs(f_step7 / 1e12 - 60.88) < 0.01 and abs(f_once7 / 1e9 - 322.1) < 0.1
+    from f_lite.vae import decoder_flops
+
+    assert abs(decoder_flops(1024, 1024) / 1e12 - 10.47) < 0.01
