@@ -51,7 +51,7 @@ extern "C" {
 int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void* v, void* o, long q_row_stride,
                           long k_row_stride, long v_row_stride, long o_row_stride, long head_stride,
                           const int* cu_seqlens_q, const int* cu_seqlens_k, int batch, int num_heads, int head_dim,
-                          int max_seqlen_q, float softmax_scale) {
+                          int max_seqlen_q, float softmax_scale, float max_score) {
   AttnParams a;
   a.q = (const bf16_t*)q;
   a.k = (const bf16_t*)k;
@@ -69,6 +69,7 @@ int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void
   a.head_dim = head_dim;
   a.max_q = max_seqlen_q;
   a.scale = softmax_scale;
+  a.max_score = max_score;
   return attn_fwd(a, (hipStream_t)stream);
 }
 

@@ -9,6 +9,9 @@ namespace flite {
 
 namespace {
 constexpr int HEAD_DIM = 256;
+// q and k are RMS-normalised per head before every DiT attention (QKNorm, model.py:180,197): |q|,|k| <= 16
+// (+ bf16 rounding), so |q.k| / sqrt(256) <= 16; 16.5 leaves margin for the rounding of q and k.
+constexpr float kQKNormScoreBound = 16.5f;
 
 bool parse_block(const std::string& name, int* idx, std::string* rest) {
   if (name.rfind("blocks.", 0) != 0) return false;
@@ -414,6 +417,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.head_dim = HEAD_DIM;
     a.max_q = T_;
     a.scale = 1.0f / sqrtf((float)HEAD_DIM);
+    a.max_score = kQKNormScoreBound;
     if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
     if (attn_fwd(a, s)) return 1;
     if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
@@ -458,6 +462,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.head_dim = HEAD_DIM;
     a.max_q = T_;
     a.scale = 1.0f / sqrtf((float)HEAD_DIM);
+    a.max_score = kQKNormScoreBound;
     if (attn_fwd(a, s)) return 1;
     if (resid(obuf_, D, b.cproj_w, D, gate_ca)) return 1;
   }

@@ -51,6 +51,9 @@ struct AttnParams {
   int B = 0, H = 0, head_dim = 0;
   int max_q = 0;              // max query length (grid size)
   float scale = 1.f;
+  // > 0: every score*scale is bounded by +-max_score (QK-normed inputs) -> fixed-shift softmax, no rescale
+  float max_score = 0.f;
+  int n_qtiles = 0;  // set by the launcher
 };
 
 int attn_fwd(const AttnParams& p, hipStream_t stream);

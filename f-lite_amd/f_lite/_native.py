@@ -53,7 +53,7 @@ SIGNATURES = {
     "flite_last_error": (_cp, []),
     "flite_version": (_i, []),
     "flite_gemm_bf16": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _vp, _i, _vp, _l, _vp, _l, _i]),
-    "flite_attn_varlen_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _f]),
+    "flite_attn_varlen_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _f, _f]),
     "flite_rmsnorm_modulate": (_i, [_vp, _vp, _i, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_rope_qknorm": (_i, [_vp, _vp, _l, _l, _i, _i, _vp, _vp, _l, _f]),
     "flite_gather_rows": (_i, [_vp, _vp, _vp, _vp, _l, _i]),
@@ -175,7 +175,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, *, out=None, epilogue=EPI_
     return out
 
 
-def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None):
+def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None, max_score=0.0):
     """flash_attn_varlen_func replacement: q [Lq, h, 256], k/v [Lk, h, 256] (row-major, any row stride)."""
     lib = load()
     Lq, H, D = q.shape
@@ -189,7 +189,7 @@ def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None):
     require_gpu(cu_k, "cu_k", torch.int32)
     st = lib.flite_attn_varlen_fwd(stream_ptr(q.device), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(),
                                    q.stride(0), k.stride(0), v.stride(0), out.stride(0), D, cu_q.data_ptr(),
-                                   cu_k.data_ptr(), cu_q.numel() - 1, H, D, max_q, scale)
+                                   cu_k.data_ptr(), cu_q.numel() - 1, H, D, max_q, scale, max_score)
     check(st, "flite_attn_varlen_fwd")
     return out
 

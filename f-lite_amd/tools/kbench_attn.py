@@ -1,0 +1,40 @@
+"""Micro-benchmark of the attention kernel at the DiT shapes (1024^2: T=4112, B=2, H=12; cross Lk=512)."""
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch
+from f_lite import _native as nat
+
+dev = "cuda"
+
+
+def run(T, Lk, H=12, iters=20, bounded=True):
+    B = 2
+    D = 256
+    q = torch.nn.functional.normalize(torch.randn(B * T, H, D, device=dev), dim=-1).mul(16).bfloat16()
+    k = torch.nn.functional.normalize(torch.randn(B * Lk, H, D, device=dev), dim=-1).mul(16).bfloat16()
+    v = torch.randn(B * Lk, H, D, device=dev).bfloat16()
+    cu_q = torch.tensor([0, T, 2 * T], dtype=torch.int32, device=dev)
+    cu_k = torch.tensor([0, Lk, 2 * Lk], dtype=torch.int32, device=dev)
+    out = torch.empty_like(q)
+    ms_ = 16.5 if bounded else 0.0
+    for _ in range(3):
+        nat.attn_varlen(q, k, v, cu_q, cu_k, T, D ** -0.5, out=out, max_score=ms_)
+    torch.cuda.synchronize()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        nat.attn_varlen(q, k, v, cu_q, cu_k, T, D ** -0.5, out=out, max_score=ms_)
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    fl = 4.0 * B * H * T * Lk * D
+    print(f"attn T={T} Lk={Lk} bounded={bounded}: {ms * 1000:.1f} us  {fl / ms / 1e9:.0f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    for b in (False, True):
+        run(4112, 4112, bounded=b)
+        run(4112, 512, bounded=b)

@@ -88,9 +88,10 @@ def _attn_ref(q, k, v, cu_q, cu_k, scale):
     return R.attention_varlen(q.float().cpu(), k.float().cpu(), v.float().cpu(), cu_q.cpu(), cu_k.cpu(), scale)
 
 
+@pytest.mark.parametrize("bounded", [False, True])
 @pytest.mark.parametrize("lens_q,lens_k", [([80, 80], None), ([272, 272], None), ([4112], None),
                                            ([100, 37], [24, 17]), ([130, 5], [512, 0]), ([64], [1])])
-def test_attention_varlen(lens_q, lens_k):
+def test_attention_varlen(lens_q, lens_k, bounded):
     H, D = 2, 256
     self_attn = lens_k is None
     lens_k = lens_q if self_attn else lens_k
@@ -101,7 +102,8 @@ def test_attention_varlen(lens_q, lens_k):
     q = R.own_rmsnorm(torch.randn(int(cu_q[-1]), H, D, device=DEV, generator=g), None).bfloat16()
     k = R.own_rmsnorm(torch.randn(max(int(cu_k[-1]), 1), H, D, device=DEV, generator=g), None).bfloat16()
     v = torch.randn(max(int(cu_k[-1]), 1), H, D, device=DEV, generator=g).bfloat16()
-    out = nat.attn_varlen(q, k, v, cu_q.to(DEV), cu_k.to(DEV), max(lens_q), D ** -0.5)
+    out = nat.attn_varlen(q, k, v, cu_q.to(DEV), cu_k.to(DEV), max(lens_q), D ** -0.5,
+                          max_score=16.5 if bounded else 0.0)
     ref = _attn_ref(q, k, v, cu_q, cu_k, D ** -0.5)
     assert rel(out, ref) < 1e-2
 
