@@ -4,14 +4,20 @@
 //
 // Replaces every nn.Linear on the DiT hot path (reference f_lite/model.py:151-156 qkv/q/context_kv/proj,
 // model.py:261-267 LigerSwiGLUMLP gate/up/down, model.py:436 context_proj, model.py:448-456 time/adaLN,
-// model.py:475 final_proj) and the patch-embed Conv2d (model.py:321, k=s=2 == GEMM over 64-vectors).
+// model.py:475 final_proj), the patch-embed Conv2d (model.py:321, k=s=2 == GEMM over 64-vectors) and, in the
+// implicit-GEMM CONV mode, the 3x3 convolutions of the VAE decoder.
 //
-// Tile 256x256x64, 512 threads = 8 waves laid out 2(M) x 4(N), each wave owns 128x64 of C.
-// Operands are staged HBM->LDS with global_load_lds (16 B/lane, lane-linear LDS image), double-buffered;
-// the bank-conflict XOR swizzle is applied on the per-lane SOURCE address and undone on the ds_read.
-// MFMA v_mfma_f32_16x16x32_bf16 is issued with W as the "A" operand and the activations as "B", so each
-// lane's accumulator holds 4 consecutive output COLUMNS of one output row: the epilogue stores 8/16 B
-// contiguous per lane and fused row-wise epilogues (gate, SwiGLU pairs) need no shuffles.
+// Tile 256x256x64, 512 threads = 8 waves laid out 2(M) x 4(N); each wave owns 128x64 of C as 8x4 tiles of
+// v_mfma_f32_16x16x32_bf16 (on random bf16 data the 16x16x32 shape holds a higher clock than 32x32x16:
+// MI355X_MICROARCH.md, DVFS item 7). W is the MFMA "A" operand and the activations the "B" operand, so each
+// lane's accumulator holds 4 consecutive output COLUMNS of one output row (8/16-B epilogue stores; row-wise
+// fused epilogues need no shuffles).
+// Operands stream HBM->LDS by LDS-DMA (16 B/lane, lane-linear image; the bank-conflict XOR swizzle is applied on
+// the per-lane SOURCE offset and undone on the ds_read), two LDS buffers, one barrier per 64-deep k-tile.
+// Fragments are register double-buffered at half-k-step granularity (W: two sets of 4; A: low/high halves of
+// 8), so every ds_read overlaps MFMAs of the previous half-step, including across the k-tile barrier.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -22,22 +28,83 @@ namespace {
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int NT = 512;
 constexpr int TILE_BYTES = BM * BK * 2;          // 32 KiB per operand tile
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;      // A + W
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;       // double buffer = 128 KiB
+// LDS: [A buf0 | A buf1 | W buf0 | W buf1]: every fragment read is a per-lane base + 16-bit immediate
+constexpr int W_REGION = 2 * TILE_BYTES;
+constexpr int LDS_BYTES = 4 * TILE_BYTES;        // 128 KiB
 
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+// 128-B tile rows (64 bf16 of K) hold 8 16-B chunks; chunk c of row r is stored at c ^ swz(r). Any 16
+// consecutive rows then cover all 16 bank slots of a 256-B bank row -> conflict-free ds_read_b128.
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
-__device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
-  __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)ldst, 16, 0, 0);
+// One k-tile of LDS-DMA for this wave: 4 A pieces (1 KiB apart in LDS) + 4 W pieces (8 KiB apart) of 1 KiB
+// (64 lanes x 16 B) by buffer_load_dwordx4 ... lds (the range check returns 0 for out-of-range offsets: conv
+// padding). A single asm block because hipcc tracks builtin LDS-DMA and then waits vmcnt(0) before every LDS
+// read it cannot prove disjoint, serialising the prefetch with the MFMAs; the waits for these copies are
+// placed by hand. `skip` (uniform) turns the block into a no-op without splitting the basic block.
+__device__ __forceinline__ void stage_dma(const i32x4& ra, unsigned sa, unsigned va0, unsigned va1, unsigned va2,
+                                          unsigned va3, const i32x4& rw, unsigned sw, unsigned vw0, unsigned vw1,
+                                          unsigned vw2, unsigned vw3, unsigned lds_a, unsigned lds_w,
+                                          unsigned skip) {
+  unsigned keep;
+  asm volatile(
+      "s_cmp_eq_u32 %[skip], 0\n\t"
+      "s_cbranch_scc0 .Lskip_dma_%=\n\t"
+      "s_mov_b32 %[keep], m0\n\t"
+      "s_mov_b32 m0, %[la]\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[va0], %[ra], %[sa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[va1], %[ra], %[sa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[va2], %[ra], %[sa] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x400\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[va3], %[ra], %[sa] offen lds\n\t"
+      "s_mov_b32 m0, %[lw]\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[vw0], %[rw], %[sw] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x2000\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[vw1], %[rw], %[sw] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x2000\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[vw2], %[rw], %[sw] offen lds\n\t"
+      "s_add_u32 m0, m0, 0x2000\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %[vw3], %[rw], %[sw] offen lds\n\t"
+      "s_mov_b32 m0, %[keep]\n"
+      ".Lskip_dma_%=:"
+      : [keep] "=&s"(keep)
+      : [skip] "s"(skip), [la] "s"(lds_a), [lw] "s"(lds_w), [ra] "s"(ra), [sa] "s"(sa), [rw] "s"(rw), [sw] "s"(sw),
+        [va0] "v"(va0), [va1] "v"(va1), [va2] "v"(va2), [va3] "v"(va3), [vw0] "v"(vw0), [vw1] "v"(vw1),
+        [vw2] "v"(vw2), [vw3] "v"(vw3)
+      : "memory", "scc");
 }
 
-__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, unsigned voff, void* ldst) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void*)ldst, 16, voff, 0, 0, 0);
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)base;
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+  r.y = __builtin_amdgcn_readfirstlane((int)(a >> 32));
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
+  r.w = 0x00020000;
+  return r;
 }
+
+__device__ __forceinline__ unsigned lds_addr_of(const void* p) {
+  return (unsigned)(unsigned long long)(const LDS_AS char*)p;
+}
+
+// sched_group_barrier masks
+constexpr int SG_MFMA = 0x008, SG_DSR = 0x100;
 
 // CONV = implicit-GEMM 3x3 convolution (pad 1) over an NHWC bf16 input: A row m = output pixel, k = (tap, c)
 // with tap = ky*3+kx. Each 64-wide k-tile is one tap and 64 consecutive channels (128 contiguous bytes of
-// one input pixel) -> staged by buffer_load ... lds, whose range check returns 0 for the padding pixels.
+// one input pixel); the buffer range check returns 0 for the padding pixels.
 // `upsample` folds nearest-2x interpolation into the addressing (Upsample2D + conv).
 template <int EPI, bool CONV>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
@@ -69,75 +136,79 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
   const int m0 = tile_m * BM;
   const int n0 = tile_n * BN;
 
-  // ---- per-lane staging sources (4 rows of A and 4 rows of W per wave per k-tile) ----
-  // glds instruction q (0..31) covers tile rows 8q..8q+7; lane -> row 8q + lane/8, 16-B chunk (lane&7)^swz.
-  const bf16_t* a_src[4];
-  const bf16_t* w_src[4];
-  int cy[4], cx[4];
-  unsigned cbase[4];  // element offset of (batch, chunk) for CONV
-  __amdgpu_buffer_rsrc_t crs;
-  if constexpr (CONV) crs = __builtin_amdgcn_make_buffer_rsrc((void*)p.conv_in, 0, (int)p.conv_in_bytes, 0x00020000);
+  // ---- per-lane staging offsets ----
+  // DMA piece q (0..31) covers tile rows 8q..8q+7; lane -> row 8q + lane/8, 16-B chunk (lane&7)^swz(row).
+  // A: wave w copies pieces 4w..4w+3; W: pieces w, w+8, w+16, w+24 (rows 8w + 64i), so that under the SwiGLU
+  // interleave (16-row sub-tiles alternate gate / up) all of a wave's W pieces come from one tensor.
+  // Both operands are addressed as buffers: per-lane byte offset of (row, chunk) + uniform k offset in soffset.
+  unsigned a_off[4], w_off[4];
+  int cyx[4];  // CONV: output pixel (y << 16 | x) of the piece's row
+  const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr_of(smem));
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int q = wave * 4 + i;
-    const int row = q * 8 + (lane >> 3);
-    const int chunk = (lane & 7) ^ swz(row);
-    const int am = min(m0 + row, p.M - 1);
-    if constexpr (CONV) {
-      const int hw = p.conv_oh * p.conv_ow;
-      const int b = am / hw;
-      const int r = am - b * hw;
-      cy[i] = r / p.conv_ow;
-      cx[i] = r - cy[i] * p.conv_ow;
-      cbase[i] = (unsigned)((long)b * p.conv_ih * p.conv_iw * p.conv_c + chunk * 8);
-      a_src[i] = nullptr;
-    } else {
-      a_src[i] = p.A + (long)am * p.lda + chunk * 8;
+    {
+      const int row = (wave * 4 + i) * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ swz(row);
+      const int am = min(m0 + row, p.M - 1);
+      if constexpr (CONV) {
+        const int hw = p.conv_oh * p.conv_ow;
+        const int b = am / hw;
+        const int r = am - b * hw;
+        const int y = r / p.conv_ow;
+        cyx[i] = (y << 16) | (r - y * p.conv_ow);
+        a_off[i] = (unsigned)((long)b * p.conv_ih * p.conv_iw * p.conv_c + chunk * 8) * 2u;
+      } else {
+        a_off[i] = (unsigned)(((long)am * p.lda + chunk * 8) * 2);
+      }
     }
-    const int wn = min(n0 + row, p.N - 1);
-    const bf16_t* wbase;
-    long wrow;
-    if constexpr (EPI == EPI_SWIGLU_BF16) {
-      // virtual row wn: 16-row sub-tiles alternate gate (W) / up (W2) rows of the same output columns
-      const int sub = wn >> 4;
-      wrow = (long)(sub >> 1) * 16 + (wn & 15);
-      wbase = (sub & 1) ? p.W2 : p.W;
-    } else {
-      wrow = wn;
-      wbase = p.W;
+    {
+      const int row = (wave + 8 * i) * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ swz(row);
+      const int wn = min(n0 + row, p.N - 1);
+      long wrow = wn;
+      if constexpr (EPI == EPI_SWIGLU_BF16) {
+        // virtual row wn: sub-tile wn>>4 is gate (even) / up (odd) of output columns (wn>>5)*16 + (wn&15)
+        wrow = (long)(wn >> 5) * 16 + (wn & 15);
+      }
+      w_off[i] = (unsigned)((wrow * p.ldw + chunk * 8) * 2);
     }
-    w_src[i] = wbase + wrow * p.ldw + chunk * 8;
   }
+  const i32x4 a_rsrc = CONV ? make_rsrc(p.conv_in, (unsigned)p.conv_in_bytes)
+                            : make_rsrc(p.A, (unsigned)((long)p.M * p.lda * 2));
+  // SwiGLU: rows 8w + 64i lie in sub-tile (w>>1) + 4i, whose parity is (w>>1)&1
+  const bf16_t* wsrc = (EPI == EPI_SWIGLU_BF16 && ((wave >> 1) & 1)) ? p.W2 : p.W;
+  const long w_rows = EPI == EPI_SWIGLU_BF16 ? (long)(p.N >> 1) : (long)p.N;
+  const i32x4 w_rsrc = make_rsrc(wsrc, (unsigned)(w_rows * p.ldw * 2));
+  const int nk = p.K / BK;
 
+  // DMA k-tile kt into LDS buffer buf (no-op when kt >= nk)
   auto stage = [&](int kt, int buf) {
-    char* base = smem + buf * STAGE_BYTES;
-    const int koff = kt * BK;
+    const unsigned la = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds0 + buf * TILE_BYTES + wave * 4096));
+    const unsigned lw = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds0 + W_REGION + buf * TILE_BYTES + wave * 1024));
+    const unsigned kb = (unsigned)(kt * BK * 2);
+    unsigned va[4];
+    unsigned sa;
     if constexpr (CONV) {
+      const int koff = kt * BK;
       const int tap = koff / p.conv_c;
       const int c0 = koff - tap * p.conv_c;
       const int ky = tap / 3 - 1, kx = tap % 3 - 1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int q = wave * 4 + i;
-        const int iy = cy[i] + ky, ix = cx[i] + kx;
+        const int iy = (cyx[i] >> 16) + ky, ix = (cyx[i] & 0xffff) + kx;
         const bool ok = iy >= 0 && iy < p.conv_oh && ix >= 0 && ix < p.conv_ow;
         const int sy = p.conv_up ? (iy >> 1) : iy;
         const int sx = p.conv_up ? (ix >> 1) : ix;
-        const unsigned e = cbase[i] + (unsigned)((sy * p.conv_iw + sx) * p.conv_c + c0);
-        blds16(crs, ok ? e * 2u : 0x80000000u, base + q * 1024);
+        va[i] = ok ? a_off[i] + (unsigned)((sy * p.conv_iw + sx) * p.conv_c + c0) * 2u : 0x80000000u;
       }
+      sa = 0;
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = wave * 4 + i;
-        glds16(a_src[i] + koff, base + q * 1024);
-      }
+      for (int i = 0; i < 4; ++i) va[i] = a_off[i];
+      sa = kb;
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = wave * 4 + i;
-      glds16(w_src[i] + koff, base + TILE_BYTES + q * 1024);
-    }
+    stage_dma(a_rsrc, sa, va[0], va[1], va[2], va[3], w_rsrc, kb, w_off[0], w_off[1], w_off[2], w_off[3], la, lw,
+              (unsigned)__builtin_amdgcn_readfirstlane(kt >= nk ? 1 : 0));
   };
 
   f32x4 acc[8][4];
@@ -146,44 +217,105 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // per-lane LDS read offsets (row = base16 + (lane&15); chunk = kk*4 + (lane>>4), swizzled)
+  // Fragment reads (16x16x32 operand map): lane l holds row (l & 15), k = 8*(l>>4) + 0..7 of the 32-deep
+  // k-step s -> 16-B chunk 4s + (l>>4) of a 128-B tile row. Rows: W tile wave_n*64 + ni*16 + (l&15),
+  // A tile wave_m*128 + mi*16 + (l&15); the swizzle depends only on l&15 (row bases are multiples of 16).
   const int lr = lane & 15;
-  const int lsw = (lr >> 1) & 7;
   const int lk = lane >> 4;
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    const char* As = smem + cur * STAGE_BYTES;
-    const char* Ws = As + TILE_BYTES;
+  unsigned ab[2], wb[2];  // per-lane LDS byte address of k-step s in buffer 0
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int coff = (((kk * 4 + lk) ^ lsw) << 4);
-      bf16x8 wf[4], af[8];
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int row = wave_n * 64 + ni * 16 + lr;
-        wf[ni] = *(const bf16x8*)(Ws + row * 128 + coff);
-      }
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const int row = wave_m * 128 + mi * 16 + lr;
-        af[mi] = *(const bf16x8*)(As + row * 128 + coff);
-      }
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[mi], acc[mi][ni], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  for (int s = 0; s < 2; ++s) {
+    const unsigned coff = ((4 * s + lk) ^ swz(lr)) << 4;
+    ab[s] = lds0 + (wave_m * 128 + lr) * 128 + coff;
+    wb[s] = lds0 + W_REGION + (wave_n * 64 + lr) * 128 + coff;
   }
+  // W fragment ni (of k-step s, buffer BUF) / A fragment mi
+  auto rd_w = [&](auto BUFC, int s, int ni) {
+    return *(const LDS_AS bf16x8*)(wb[s] + decltype(BUFC)::value * TILE_BYTES + ni * 16 * 128);
+  };
+  auto rd_a = [&](auto BUFC, int s, int mi) {
+    return *(const LDS_AS bf16x8*)(ab[s] + decltype(BUFC)::value * TILE_BYTES + mi * 16 * 128);
+  };
+  // 16 MFMAs: A rows mi0..mi0+3 x all 4 W fragments
+  auto mfma_half = [&](const bf16x8(&wf)[4], const bf16x8(&af)[4], int mi0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        acc[mi0 + i][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[i], acc[mi0 + i][ni], 0, 0, 0);
+  };
+  // spread `nr` ds_reads over a half-step's 16 MFMAs
+  auto interleave = [&](auto NR) {
+    constexpr int nr = decltype(NR)::value;
+    constexpr int per = 16 / nr;
+#pragma unroll
+    for (int i = 0; i < nr; ++i) {
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, per, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(SG_MFMA, 16 - per * nr, 0);
+  };
+  using I4 = std::integral_constant<int, 4>;
+  using I6 = std::integral_constant<int, 6>;
+  using I8 = std::integral_constant<int, 8>;
+
+  // Pipeline over 64-deep k-tiles (tile t lives in LDS buffer t&1; tile t+1 is in flight). Register sets:
+  // wx / wy = W fragments of alternating k-steps, al / ah = A fragments mi 0..3 / 4..7.
+  //   k0.lo: MFMA(wx, al) || read ah(k0), wy[0..1](k1)      k0.hi: MFMA(wx, ah) || read wy[2..3](k1), al(k1)
+  //   k1.lo: MFMA(wy, al) || read ah(k1)
+  //   wait for tile t+1 (own copies) + all reads of buffer t&1, barrier, DMA tile t+2 into buffer t&1
+  //   k1.hi: MFMA(wy, ah) || read wx, al of k0 of tile t+1 (stale, unused data after the last tile)
+  // Every tile runs the same straight-line code; the loop is unrolled x2 so the buffer index is static.
+  stage(0, 0);
+  stage(1, 1);
+  if (nk > 1)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's 8 copies of tile 0 (tile 1's may fly)
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  bf16x8 wx[4], wy[4], al[4], ah[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    wx[i] = rd_w(B0{}, 0, i);
+    al[i] = rd_a(B0{}, 0, i);
+  }
+  auto tile = [&](auto BUFC, int kt) {
+    using NXT = std::integral_constant<int, decltype(BUFC)::value ^ 1>;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ah[i] = rd_a(BUFC, 0, 4 + i);
+    wy[0] = rd_w(BUFC, 1, 0);
+    wy[1] = rd_w(BUFC, 1, 1);
+    mfma_half(wx, al, 0);
+    interleave(I6{});
+    wy[2] = rd_w(BUFC, 1, 2);
+    wy[3] = rd_w(BUFC, 1, 3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) al[i] = rd_a(BUFC, 1, i);
+    mfma_half(wx, ah, 4);
+    interleave(I6{});
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ah[i] = rd_a(BUFC, 1, 4 + i);
+    mfma_half(wy, al, 0);
+    interleave(I4{});
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stage(kt + 2, decltype(BUFC)::value);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wx[i] = rd_w(NXT{}, 0, i);
+      al[i] = rd_a(NXT{}, 0, i);
+    }
+    mfma_half(wy, ah, 4);
+    interleave(I8{});
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    tile(B0{}, kt);
+    tile(B1{}, kt + 1);
+  }
+  if (kt < nk) tile(B0{}, kt);
 
   // ---- epilogue: lane holds C[m][n..n+3] for m = m_base + mi*16 + (lane&15), n = n_base + ni*16 + 4*(lane>>4)
   const int m_base = m0 + wave_m * 128 + lr;
@@ -320,6 +452,7 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
   FLITE_REQUIRE(p.K % BK == 0, "gemm: K must be a multiple of 64");
   FLITE_REQUIRE(p.ldw % 8 == 0, "gemm: ldw must be a multiple of 8 elements");
   FLITE_REQUIRE(((uintptr_t)p.W & 15) == 0, "gemm: W must be 16-B aligned");
+  FLITE_REQUIRE((long)p.N * p.ldw * 2 < (1L << 32), "gemm: W must be < 4 GiB (32-bit buffer offsets)");
   if (p.conv_in != nullptr) {
     FLITE_REQUIRE(p.conv_c % 64 == 0, "conv: input channels must be a multiple of 64");
     FLITE_REQUIRE(p.K == 9 * p.conv_c, "conv: K must be 9 * C_in");
@@ -329,6 +462,7 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
     FLITE_REQUIRE(epi == EPI_STORE_BF16 || epi == EPI_STORE_F32, "conv: store epilogues only");
   } else {
     FLITE_REQUIRE(p.lda % 8 == 0, "gemm: lda must be a multiple of 8 elements");
+    FLITE_REQUIRE((long)p.M * p.lda * 2 < (1L << 32), "gemm: A must be < 4 GiB (32-bit buffer offsets)");
     FLITE_REQUIRE(((uintptr_t)p.A & 15) == 0, "gemm: A must be 16-B aligned");
   }
   if (gemm_init()) return 1;
