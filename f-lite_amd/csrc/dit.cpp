@@ -36,11 +36,19 @@ DitEngine::DitEngine(const flite_dit_config& c) : cfg(c) {
 }
 
 DitEngine::~DitEngine() {
+  drop_graph();
   free_ws();
-  if (gexec_) hipGraphExecDestroy(gexec_);
   if (gstream_) hipStreamDestroy(gstream_);
   if (ev_in_) hipEventDestroy(ev_in_);
   if (ev_out_) hipEventDestroy(ev_out_);
+}
+
+// Destroy the cached graph once every replay of it has finished (a replay may still be in flight on gstream_).
+void DitEngine::drop_graph() {
+  if (!gexec_) return;
+  if (gstream_) hipStreamSynchronize(gstream_);
+  hipGraphExecDestroy(gexec_);
+  gexec_ = nullptr;
 }
 
 void DitEngine::free_ws() {
@@ -144,11 +152,8 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   FLITE_REQUIRE(cfg.cross_attn_input_size % 64 == 0, "config: cross_attn_input_size must be a multiple of 64");
   if (check_bound()) return 2;
   if (B == B_ && Hl == Hl_ && Wl == Wl_ && n_ctx_max <= nctx_max_ && n_t_max <= ntmax_) return 0;
+  drop_graph();
   free_ws();
-  if (gexec_) {
-    hipGraphExecDestroy(gexec_);
-    gexec_ = nullptr;
-  }
   B_ = B;
   Hl_ = Hl;
   Wl_ = Wl;
@@ -165,6 +170,7 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   if (alloc((void**)&hbuf_, M_ * (long)F * 2)) return 1;
   if (alloc((void**)&patches_, (long)B * HW_ * cpp * 2)) return 1;
   if (alloc((void**)&fout_, (long)B * HW_ * cpp * 4)) return 1;
+  if (alloc((void**)&acc_, (long)B * HW_ * cpp * 4)) return 1;
   if (alloc((void**)&cu_self_, (B + 1) * 4)) return 1;
   if (alloc((void**)&cu_ctx_, (B + 1) * 4)) return 1;
   if (alloc((void**)&cos_, (long)T_ * 128 * 4)) return 1;
@@ -496,10 +502,7 @@ int DitEngine::set_probe(int kind, int max_pairs) {
   probe_ev_.clear();
   probe_n_ = 0;
   probe_kind_ = kind;
-  if (gexec_) {  // a cached graph holds (or lacks) the old probe nodes
-    hipGraphExecDestroy(gexec_);
-    gexec_ = nullptr;
-  }
+  drop_graph();  // a cached graph holds (or lacks) the old probe nodes
   if (kind < 0) return 0;
   FLITE_REQUIRE(max_pairs > 0 && max_pairs <= 100000, "set_probe: bad max_pairs");
   probe_ev_.resize(2 * (size_t)max_pairs);
@@ -608,7 +611,7 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
   FLITE_HIP_CHECK(hipMemcpyAsync(tdev_, t_host, n_steps * 4, hipMemcpyHostToDevice, s));
   if (set_timesteps(s, tdev_, n_steps, cfg.bf16_timestep_quant)) return 1;
 
-  auto body = [&](hipStream_t st) -> int {
+  auto body = [&](hipStream_t st, float* acc) -> int {
     probe_n_ = 0;
     for (int i = 0; i < n_steps; ++i) {
       if (probe_begin(st, FLITE_PROBE_STEP)) return 1;
@@ -622,9 +625,10 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
     }
     return 0;
   };
-  if (!use_graph) return body(s);
+  if (!use_graph) return body(s, acc);
 
-  // hipGraph: capture the whole n_steps loop once per (shape, schedule, guidance, accumulator), replay after
+  // hipGraph: capture the whole n_steps loop once per (shape, schedule, guidance), replay after. The graph
+  // integrates into the engine-owned accumulator acc_, so the caller's buffer address does not key the graph.
   std::vector<float> key = {(float)n_steps, guidance, (float)use_cfg, (float)apg, apg_thr};
   for (int i = 0; i < n_steps; ++i) key.push_back(dt_host[i]);
   if (!gstream_) {
@@ -632,27 +636,26 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
     FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
   }
+  const size_t acc_bytes = (size_t)Bi * HW_ * C * P * P * 4;
+  FLITE_HIP_CHECK(hipMemcpyAsync(acc_, acc, acc_bytes, hipMemcpyDeviceToDevice, s));
   FLITE_HIP_CHECK(hipEventRecord(ev_in_, s));
   FLITE_HIP_CHECK(hipStreamWaitEvent(gstream_, ev_in_, 0));
-  if (!gexec_ || key != gkey_ || glat_ != acc) {
-    if (gexec_) {
-      hipGraphExecDestroy(gexec_);
-      gexec_ = nullptr;
-    }
+  if (!gexec_ || key != gkey_) {
+    drop_graph();
     hipGraph_t graph;
     FLITE_HIP_CHECK(hipStreamBeginCapture(gstream_, hipStreamCaptureModeThreadLocal));
-    const int rc = body(gstream_);
+    const int rc = body(gstream_, acc_);
     const hipError_t e = hipStreamEndCapture(gstream_, &graph);
     if (rc) return rc;
     FLITE_HIP_CHECK(e);
     FLITE_HIP_CHECK(hipGraphInstantiate(&gexec_, graph, nullptr, nullptr, 0));
     hipGraphDestroy(graph);
     gkey_ = key;
-    glat_ = acc;
   }
   FLITE_HIP_CHECK(hipGraphLaunch(gexec_, gstream_));
   FLITE_HIP_CHECK(hipEventRecord(ev_out_, gstream_));
   FLITE_HIP_CHECK(hipStreamWaitEvent(s, ev_out_, 0));
+  FLITE_HIP_CHECK(hipMemcpyAsync(acc, acc_, acc_bytes, hipMemcpyDeviceToDevice, s));
   return 0;
 }
 

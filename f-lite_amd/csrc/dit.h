@@ -64,6 +64,7 @@ class DitEngine {
   int run_block(hipStream_t s, int blk, const float* mod, long mseg);
   int alloc(void** p, size_t bytes);
   void free_ws();
+  void drop_graph();
 
   DitW w_;
   std::map<std::string, std::pair<const void*, long>> bound_;
@@ -76,6 +77,7 @@ class DitEngine {
   float* x_ = nullptr;
   bf16_t *nbuf_ = nullptr, *qkv_ = nullptr, *obuf_ = nullptr, *hbuf_ = nullptr, *patches_ = nullptr;
   float* fout_ = nullptr;
+  float* acc_ = nullptr;  // graph-owned Euler accumulator (sample)
   int *cu_self_ = nullptr, *cu_ctx_ = nullptr;
   float *cos_ = nullptr, *sin_ = nullptr, *inv_freq_ = nullptr;
   bf16_t* ctx_p_ = nullptr;
@@ -93,7 +95,6 @@ class DitEngine {
   hipGraphExec_t gexec_ = nullptr;
   std::vector<float> gkey_;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
-  const void* glat_ = nullptr;
 };
 
 }  // namespace flite
