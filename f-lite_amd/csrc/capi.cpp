@@ -43,6 +43,34 @@ int flite_gemm_bf16(void* stream, int M, int N, int K, const void* A, long lda, 
   return gemm_bf16(p, epilogue, (hipStream_t)stream);
 }
 
+long flite_gemm_workspace_bytes(void) { return (long)gemm_sk_workspace_bytes(); }
+
+int flite_gemm_bf16_ws(void* stream, int M, int N, int K, const void* A, long lda, const void* W, long ldw,
+                       const void* W2, const void* bias, int epilogue, void* out, long ldo, const float* gate,
+                       long gate_seg_stride, int rows_per_seg, void* workspace) {
+  GemmParams p;
+  p.A = (const bf16_t*)A;
+  p.lda = lda;
+  p.W = (const bf16_t*)W;
+  p.ldw = ldw;
+  p.W2 = (const bf16_t*)W2;
+  p.bias = (const bf16_t*)bias;
+  p.out = out;
+  p.ldo = ldo;
+  p.gate = gate;
+  p.gate_seg_stride = gate_seg_stride;
+  p.rows_per_seg = rows_per_seg;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  const int G = gemm_sk_workspace_cus();
+  if (workspace != nullptr && G > 0) {
+    p.sk_ws = (float*)workspace;
+    p.sk_flags = (int*)((char*)workspace + (size_t)G * 256 * 256 * 4);
+  }
+  return gemm_bf16(p, epilogue, (hipStream_t)stream);
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------------------------------

@@ -1,6 +1,8 @@
 // Native DiT engine (host side). See dit.h.
 #include "dit.h"
 
+#include <cstdlib>
+
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -55,6 +57,14 @@ void DitEngine::free_ws() {
   for (void* p : allocs_) hipFree(p);
   allocs_.clear();
   ctx_kv_.clear();
+}
+
+// every GEMM of the engine may use the stream-K workspace (launches on the engine's streams are ordered)
+int DitEngine::gemm(GemmParams& g, int epi, hipStream_t s) {
+  static const bool no_sk = getenv("FLITE_GEMM_NO_STREAM_K") != nullptr;  // A/B switch for measurements
+  g.sk_ws = no_sk ? nullptr : sk_ws_;
+  g.sk_flags = no_sk ? nullptr : sk_flags_;
+  return gemm_bf16(g, epi, s);
 }
 
 int DitEngine::alloc(void** p, size_t bytes) {
@@ -171,6 +181,14 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   if (alloc((void**)&patches_, (long)B * HW_ * cpp * 2)) return 1;
   if (alloc((void**)&fout_, (long)B * HW_ * cpp * 4)) return 1;
   if (alloc((void**)&acc_, (long)B * HW_ * cpp * 4)) return 1;
+  {
+    const int G = gemm_sk_workspace_cus();
+    if (G > 0) {
+      if (alloc((void**)&sk_ws_, (size_t)G * 256 * 256 * 4)) return 1;
+      if (alloc((void**)&sk_flags_, (size_t)G * 4)) return 1;
+      FLITE_HIP_CHECK(hipMemset(sk_flags_, 0, (size_t)G * 4));
+    }
+  }
   if (alloc((void**)&cu_self_, (B + 1) * 4)) return 1;
   if (alloc((void**)&cu_ctx_, (B + 1) * 4)) return 1;
   if (alloc((void**)&cos_, (long)T_ * 128 * 4)) return 1;
@@ -228,7 +246,7 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
   g.M = n;
   g.N = D;
   g.K = cfg.cross_attn_input_size;
-  if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+  if (gemm(g, EPI_STORE_BF16, s)) return 1;
   NormModParams nm;
   nm.x = ctx_p_;
   nm.ldx = D;
@@ -253,7 +271,7 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
     k.M = n;
     k.N = 2 * D;
     k.K = D;
-    if (gemm_bf16(k, EPI_STORE_BF16, s)) return 1;
+    if (gemm(k, EPI_STORE_BF16, s)) return 1;
     RopeNormParams rn;
     rn.x = ctx_kv_[i];
     rn.ldx = 2L * D;
@@ -284,7 +302,7 @@ int DitEngine::set_timesteps(hipStream_t s, const float* t_dev, int n, int quant
   g.N = 4 * D;
   g.K = D;
   g.act = 1;
-  if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+  if (gemm(g, EPI_STORE_BF16, s)) return 1;
   GemmParams g2;
   g2.A = th_;
   g2.lda = 4L * D;
@@ -297,7 +315,7 @@ int DitEngine::set_timesteps(hipStream_t s, const float* t_dev, int n, int quant
   g2.N = D;
   g2.K = 4 * D;
   g2.act = 1;
-  if (gemm_bf16(g2, EPI_STORE_BF16, s)) return 1;
+  if (gemm(g2, EPI_STORE_BF16, s)) return 1;
   // adaLN modulation rows (model.py:553-556; model_v2.py:275 per block), fp32
   auto ada = [&](const bf16_t* W, const bf16_t* b, float* out, long ldo) -> int {
     GemmParams a;
@@ -311,7 +329,7 @@ int DitEngine::set_timesteps(hipStream_t s, const float* t_dev, int n, int quant
     a.M = n;
     a.N = 9 * D;
     a.K = D;
-    return gemm_bf16(a, EPI_STORE_F32, s);
+    return gemm(a, EPI_STORE_F32, s);
   };
   if (cfg.per_block_adaln) {
     for (int i = 0; i < cfg.depth; ++i)
@@ -331,7 +349,7 @@ int DitEngine::set_timesteps(hipStream_t s, const float* t_dev, int n, int quant
   f.M = n;
   f.N = 2 * D;
   f.K = D;
-  if (gemm_bf16(f, EPI_STORE_F32, s)) return 1;
+  if (gemm(f, EPI_STORE_F32, s)) return 1;
   return 0;
 }
 
@@ -374,7 +392,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.M = (int)M_;
     g.N = D;
     g.K = K;
-    return gemm_bf16(g, EPI_RESID_F32, s);
+    return gemm(g, EPI_RESID_F32, s);
   };
 
   // --- self attention ---
@@ -392,7 +410,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.N = 3 * D;
     g.K = D;
     if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
-    if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+    if (gemm(g, EPI_STORE_BF16, s)) return 1;
     if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
   }
   {
@@ -444,7 +462,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.M = (int)M_;
     g.N = D;
     g.K = D;
-    if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
+    if (gemm(g, EPI_STORE_BF16, s)) return 1;
     RopeNormParams rn;
     rn.x = qkv_;
     rn.ldx = D;
@@ -488,7 +506,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.N = 2 * F;
     g.K = D;
     if (probe_begin(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
-    if (gemm_bf16(g, EPI_SWIGLU_BF16, s)) return 1;
+    if (gemm(g, EPI_SWIGLU_BF16, s)) return 1;
     if (probe_end(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
   }
   if (probe_begin(s, FLITE_PROBE_GEMM_DOWN)) return 1;
@@ -556,7 +574,7 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     g.out_seg = HW_;
     g.out_seg_stride = T_;
     g.out_seg_off = R;
-    if (gemm_bf16(g, EPI_STORE_F32, s)) return 1;
+    if (gemm(g, EPI_STORE_F32, s)) return 1;
   }
   if (fill_registers(x_, w_.registers, B_, T_, R, D, s)) return 1;
   const long mseg = (long)t_row_step * mod_t_stride_;
@@ -592,7 +610,7 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     g.M = B_ * HW_;
     g.N = cpp;
     g.K = D;
-    if (gemm_bf16(g, EPI_STORE_F32, s)) return 1;
+    if (gemm(g, EPI_STORE_F32, s)) return 1;
   }
   return 0;
 }

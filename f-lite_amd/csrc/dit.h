@@ -65,6 +65,7 @@ class DitEngine {
   int alloc(void** p, size_t bytes);
   void free_ws();
   void drop_graph();
+  int gemm(GemmParams& g, int epi, hipStream_t s);
 
   DitW w_;
   std::map<std::string, std::pair<const void*, long>> bound_;
@@ -78,6 +79,8 @@ class DitEngine {
   bf16_t *nbuf_ = nullptr, *qkv_ = nullptr, *obuf_ = nullptr, *hbuf_ = nullptr, *patches_ = nullptr;
   float* fout_ = nullptr;
   float* acc_ = nullptr;  // graph-owned Euler accumulator (sample)
+  float* sk_ws_ = nullptr;  // stream-K GEMM partial tiles
+  int* sk_flags_ = nullptr;
   int *cu_self_ = nullptr, *cu_ctx_ = nullptr;
   float *cos_ = nullptr, *sin_ = nullptr, *inv_freq_ = nullptr;
   bf16_t* ctx_p_ = nullptr;

@@ -107,84 +107,84 @@ constexpr int SG_MFMA = 0x008, SG_DSR = 0x100;
 // one input pixel); the buffer range check returns 0 for the padding pixels.
 // `upsample` folds nearest-2x interpolation into the addressing (Upsample2D + conv).
 template <int EPI, bool CONV>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wave_m = wave >> 2;  // 0..1
-  const int wave_n = wave & 3;   // 0..3
+struct GemmCta {
+  const GemmParams& p;
+  int tid, lane, wave, wave_m, wave_n, lr, lk;
+  unsigned lds0;
+  i32x4 a_rsrc, w_rsrc;
+  unsigned ab[2], wb[2];  // per-lane LDS byte address of k-step s in buffer 0 (row base + swizzled chunk)
+  // per output tile
+  unsigned a_off[4], w_off[4];
+  int cyx[4];  // CONV: output pixel (y << 16 | x) of the piece's row
+  int ke;      // end of the k-tile range being staged
 
-  // ---- tile scheduling: XCD-aware bijective remap, then grouped (M-fastest) ordering ----
-  const int num_m = (p.M + BM - 1) / BM;
-  const int num_n = (p.N + BN - 1) / BN;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  int wg;
-  {
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  __device__ __forceinline__ GemmCta(const GemmParams& p_, char* smem) : p(p_) {
+    tid = threadIdx.x;
+    lane = tid & 63;
+    wave = tid >> 6;
+    wave_m = wave >> 2;  // 0..1
+    wave_n = wave & 3;   // 0..3
+    lr = lane & 15;
+    lk = lane >> 4;
+    lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr_of(smem));
+    a_rsrc = CONV ? make_rsrc(p.conv_in, (unsigned)p.conv_in_bytes) : make_rsrc(p.A, (unsigned)((long)p.M * p.lda * 2));
+    // SwiGLU: W rows 8w + 64i lie in 16-row sub-tile (w>>1) + 4i, whose parity (gate / up) is (w>>1)&1
+    const bf16_t* wsrc = (EPI == EPI_SWIGLU_BF16 && ((wave >> 1) & 1)) ? p.W2 : p.W;
+    const long w_rows = EPI == EPI_SWIGLU_BF16 ? (long)(p.N >> 1) : (long)p.N;
+    w_rsrc = make_rsrc(wsrc, (unsigned)(w_rows * p.ldw * 2));
+    // Fragment reads (16x16x32 operand map): lane l holds row (l & 15), k = 8*(l>>4) + 0..7 of the 32-deep
+    // k-step s -> 16-B chunk 4s + (l>>4) of a 128-B tile row. Rows: W tile wave_n*64 + ni*16 + (l&15),
+    // A tile wave_m*128 + mi*16 + (l&15); the swizzle depends only on l&15 (row bases are multiples of 16).
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const unsigned coff = ((4 * s + lk) ^ swz(lr)) << 4;
+      ab[s] = lds0 + (wave_m * 128 + lr) * 128 + coff;
+      wb[s] = lds0 + W_REGION + (wave_n * 64 + lr) * 128 + coff;
+    }
   }
-  constexpr int GROUP = 8;
-  const int group_size = GROUP * num_n;
-  const int gid = wg / group_size;
-  const int first_m = gid * GROUP;
-  const int gm = min(num_m - first_m, GROUP);
-  const int rem = wg - gid * group_size;
-  const int tile_m = first_m + rem % gm;
-  const int tile_n = rem / gm;
-  const int m0 = tile_m * BM;
-  const int n0 = tile_n * BN;
 
-  // ---- per-lane staging offsets ----
+  // Per-lane staging offsets of output tile (m0, n0).
   // DMA piece q (0..31) covers tile rows 8q..8q+7; lane -> row 8q + lane/8, 16-B chunk (lane&7)^swz(row).
   // A: wave w copies pieces 4w..4w+3; W: pieces w, w+8, w+16, w+24 (rows 8w + 64i), so that under the SwiGLU
   // interleave (16-row sub-tiles alternate gate / up) all of a wave's W pieces come from one tensor.
   // Both operands are addressed as buffers: per-lane byte offset of (row, chunk) + uniform k offset in soffset.
-  unsigned a_off[4], w_off[4];
-  int cyx[4];  // CONV: output pixel (y << 16 | x) of the piece's row
-  const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr_of(smem));
+  __device__ __forceinline__ void setup_tile(int m0, int n0) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    {
-      const int row = (wave * 4 + i) * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ swz(row);
-      const int am = min(m0 + row, p.M - 1);
-      if constexpr (CONV) {
-        const int hw = p.conv_oh * p.conv_ow;
-        const int b = am / hw;
-        const int r = am - b * hw;
-        const int y = r / p.conv_ow;
-        cyx[i] = (y << 16) | (r - y * p.conv_ow);
-        a_off[i] = (unsigned)((long)b * p.conv_ih * p.conv_iw * p.conv_c + chunk * 8) * 2u;
-      } else {
-        a_off[i] = (unsigned)(((long)am * p.lda + chunk * 8) * 2);
+    for (int i = 0; i < 4; ++i) {
+      {
+        const int row = (wave * 4 + i) * 8 + (lane >> 3);
+        const int chunk = (lane & 7) ^ swz(row);
+        const int am = min(m0 + row, p.M - 1);
+        if constexpr (CONV) {
+          const int hw = p.conv_oh * p.conv_ow;
+          const int b = am / hw;
+          const int r = am - b * hw;
+          const int y = r / p.conv_ow;
+          cyx[i] = (y << 16) | (r - y * p.conv_ow);
+          a_off[i] = (unsigned)((long)b * p.conv_ih * p.conv_iw * p.conv_c + chunk * 8) * 2u;
+        } else {
+          a_off[i] = (unsigned)(((long)am * p.lda + chunk * 8) * 2);
+        }
       }
-    }
-    {
-      const int row = (wave + 8 * i) * 8 + (lane >> 3);
-      const int chunk = (lane & 7) ^ swz(row);
-      const int wn = min(n0 + row, p.N - 1);
-      long wrow = wn;
-      if constexpr (EPI == EPI_SWIGLU_BF16) {
-        // virtual row wn: sub-tile wn>>4 is gate (even) / up (odd) of output columns (wn>>5)*16 + (wn&15)
-        wrow = (long)(wn >> 5) * 16 + (wn & 15);
+      {
+        const int row = (wave + 8 * i) * 8 + (lane >> 3);
+        const int chunk = (lane & 7) ^ swz(row);
+        const int wn = min(n0 + row, p.N - 1);
+        long wrow = wn;
+        if constexpr (EPI == EPI_SWIGLU_BF16) {
+          // virtual row wn: sub-tile wn>>4 is gate (even) / up (odd) of output columns (wn>>5)*16 + (wn&15)
+          wrow = (long)(wn >> 5) * 16 + (wn & 15);
+        }
+        w_off[i] = (unsigned)((wrow * p.ldw + chunk * 8) * 2);
       }
-      w_off[i] = (unsigned)((wrow * p.ldw + chunk * 8) * 2);
     }
   }
-  const i32x4 a_rsrc = CONV ? make_rsrc(p.conv_in, (unsigned)p.conv_in_bytes)
-                            : make_rsrc(p.A, (unsigned)((long)p.M * p.lda * 2));
-  // SwiGLU: rows 8w + 64i lie in sub-tile (w>>1) + 4i, whose parity is (w>>1)&1
-  const bf16_t* wsrc = (EPI == EPI_SWIGLU_BF16 && ((wave >> 1) & 1)) ? p.W2 : p.W;
-  const long w_rows = EPI == EPI_SWIGLU_BF16 ? (long)(p.N >> 1) : (long)p.N;
-  const i32x4 w_rsrc = make_rsrc(wsrc, (unsigned)(w_rows * p.ldw * 2));
-  const int nk = p.K / BK;
 
-  // DMA k-tile kt into LDS buffer buf (no-op when kt >= nk)
-  auto stage = [&](int kt, int buf) {
+  // DMA k-tile kt into LDS buffer buf (no-op when kt >= ke)
+  __device__ __forceinline__ void stage(int kt, int buf) {
     const unsigned la = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds0 + buf * TILE_BYTES + wave * 4096));
-    const unsigned lw = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds0 + W_REGION + buf * TILE_BYTES + wave * 1024));
+    const unsigned lw =
+        (unsigned)__builtin_amdgcn_readfirstlane((int)(lds0 + W_REGION + buf * TILE_BYTES + wave * 1024));
     const unsigned kb = (unsigned)(kt * BK * 2);
     unsigned va[4];
     unsigned sa;
@@ -208,215 +208,370 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
       sa = kb;
     }
     stage_dma(a_rsrc, sa, va[0], va[1], va[2], va[3], w_rsrc, kb, w_off[0], w_off[1], w_off[2], w_off[3], la, lw,
-              (unsigned)__builtin_amdgcn_readfirstlane(kt >= nk ? 1 : 0));
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // Fragment reads (16x16x32 operand map): lane l holds row (l & 15), k = 8*(l>>4) + 0..7 of the 32-deep
-  // k-step s -> 16-B chunk 4s + (l>>4) of a 128-B tile row. Rows: W tile wave_n*64 + ni*16 + (l&15),
-  // A tile wave_m*128 + mi*16 + (l&15); the swizzle depends only on l&15 (row bases are multiples of 16).
-  const int lr = lane & 15;
-  const int lk = lane >> 4;
-  unsigned ab[2], wb[2];  // per-lane LDS byte address of k-step s in buffer 0
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const unsigned coff = ((4 * s + lk) ^ swz(lr)) << 4;
-    ab[s] = lds0 + (wave_m * 128 + lr) * 128 + coff;
-    wb[s] = lds0 + W_REGION + (wave_n * 64 + lr) * 128 + coff;
+              (unsigned)__builtin_amdgcn_readfirstlane(kt >= ke ? 1 : 0));
   }
-  // W fragment ni (of k-step s, buffer BUF) / A fragment mi
-  auto rd_w = [&](auto BUFC, int s, int ni) {
-    return *(const LDS_AS bf16x8*)(wb[s] + decltype(BUFC)::value * TILE_BYTES + ni * 16 * 128);
-  };
-  auto rd_a = [&](auto BUFC, int s, int mi) {
-    return *(const LDS_AS bf16x8*)(ab[s] + decltype(BUFC)::value * TILE_BYTES + mi * 16 * 128);
-  };
+
+  // W fragment ni / A fragment mi of k-step s in buffer BUF
+  template <int BUF>
+  __device__ __forceinline__ bf16x8 rd_w(int s, int ni) const {
+    return *(const LDS_AS bf16x8*)(wb[s] + BUF * TILE_BYTES + ni * 16 * 128);
+  }
+  template <int BUF>
+  __device__ __forceinline__ bf16x8 rd_a(int s, int mi) const {
+    return *(const LDS_AS bf16x8*)(ab[s] + BUF * TILE_BYTES + mi * 16 * 128);
+  }
   // 16 MFMAs: A rows mi0..mi0+3 x all 4 W fragments
-  auto mfma_half = [&](const bf16x8(&wf)[4], const bf16x8(&af)[4], int mi0) {
+  __device__ __forceinline__ static void mfma_half(f32x4 (&acc)[8][4], const bf16x8 (&wf)[4],
+                                                   const bf16x8 (&af)[4], int mi0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
         acc[mi0 + i][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[i], acc[mi0 + i][ni], 0, 0, 0);
-  };
-  // spread `nr` ds_reads over a half-step's 16 MFMAs
-  auto interleave = [&](auto NR) {
-    constexpr int nr = decltype(NR)::value;
-    constexpr int per = 16 / nr;
+  }
+  // spread NR ds_reads over a half-step's 16 MFMAs
+  template <int NR>
+  __device__ __forceinline__ static void interleave() {
+    constexpr int per = 16 / NR;
 #pragma unroll
-    for (int i = 0; i < nr; ++i) {
+    for (int i = 0; i < NR; ++i) {
       __builtin_amdgcn_sched_group_barrier(SG_MFMA, per, 0);
       __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(SG_MFMA, 16 - per * nr, 0);
-  };
-  using I4 = std::integral_constant<int, 4>;
-  using I6 = std::integral_constant<int, 6>;
-  using I8 = std::integral_constant<int, 8>;
+    __builtin_amdgcn_sched_group_barrier(SG_MFMA, 16 - per * NR, 0);
+  }
 
-  // Pipeline over 64-deep k-tiles (tile t lives in LDS buffer t&1; tile t+1 is in flight). Register sets:
-  // wx / wy = W fragments of alternating k-steps, al / ah = A fragments mi 0..3 / 4..7.
+  // One 64-deep k-tile from LDS buffer BUF. Register sets: wx / wy = W fragments of alternating k-steps,
+  // al / ah = A fragments mi 0..3 / 4..7.
   //   k0.lo: MFMA(wx, al) || read ah(k0), wy[0..1](k1)      k0.hi: MFMA(wx, ah) || read wy[2..3](k1), al(k1)
   //   k1.lo: MFMA(wy, al) || read ah(k1)
   //   wait for tile t+1 (own copies) + all reads of buffer t&1, barrier, DMA tile t+2 into buffer t&1
   //   k1.hi: MFMA(wy, ah) || read wx, al of k0 of tile t+1 (stale, unused data after the last tile)
-  // Every tile runs the same straight-line code; the loop is unrolled x2 so the buffer index is static.
-  stage(0, 0);
-  stage(1, 1);
-  if (nk > 1)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's 8 copies of tile 0 (tile 1's may fly)
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  using B0 = std::integral_constant<int, 0>;
-  using B1 = std::integral_constant<int, 1>;
-  bf16x8 wx[4], wy[4], al[4], ah[4];
+  template <int BUF>
+  __device__ __forceinline__ void ktile(f32x4 (&acc)[8][4], bf16x8 (&wx)[4], bf16x8 (&wy)[4], bf16x8 (&al)[4],
+                                        bf16x8 (&ah)[4], int kt) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    wx[i] = rd_w(B0{}, 0, i);
-    al[i] = rd_a(B0{}, 0, i);
-  }
-  auto tile = [&](auto BUFC, int kt) {
-    using NXT = std::integral_constant<int, decltype(BUFC)::value ^ 1>;
+    for (int i = 0; i < 4; ++i) ah[i] = rd_a<BUF>(0, 4 + i);
+    wy[0] = rd_w<BUF>(1, 0);
+    wy[1] = rd_w<BUF>(1, 1);
+    mfma_half(acc, wx, al, 0);
+    interleave<6>();
+    wy[2] = rd_w<BUF>(1, 2);
+    wy[3] = rd_w<BUF>(1, 3);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ah[i] = rd_a(BUFC, 0, 4 + i);
-    wy[0] = rd_w(BUFC, 1, 0);
-    wy[1] = rd_w(BUFC, 1, 1);
-    mfma_half(wx, al, 0);
-    interleave(I6{});
-    wy[2] = rd_w(BUFC, 1, 2);
-    wy[3] = rd_w(BUFC, 1, 3);
+    for (int i = 0; i < 4; ++i) al[i] = rd_a<BUF>(1, i);
+    mfma_half(acc, wx, ah, 4);
+    interleave<6>();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) al[i] = rd_a(BUFC, 1, i);
-    mfma_half(wx, ah, 4);
-    interleave(I6{});
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ah[i] = rd_a(BUFC, 1, 4 + i);
-    mfma_half(wy, al, 0);
-    interleave(I4{});
+    for (int i = 0; i < 4; ++i) ah[i] = rd_a<BUF>(1, 4 + i);
+    mfma_half(acc, wy, al, 0);
+    interleave<4>();
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    stage(kt + 2, decltype(BUFC)::value);
+    stage(kt + 2, BUF);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      wx[i] = rd_w(NXT{}, 0, i);
-      al[i] = rd_a(NXT{}, 0, i);
+      wx[i] = rd_w<BUF ^ 1>(0, i);
+      al[i] = rd_a<BUF ^ 1>(0, i);
     }
-    mfma_half(wy, ah, 4);
-    interleave(I8{});
-  };
-  int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    tile(B0{}, kt);
-    tile(B1{}, kt + 1);
+    mfma_half(acc, wy, ah, 4);
+    interleave<8>();
   }
-  if (kt < nk) tile(B0{}, kt);
+
+  // acc = A[m0.., kb*64 : kend*64] . W[n0.., same]^T  (setup_tile(m0, n0) first). Every k-tile runs the same
+  // straight-line code; the loop is unrolled x2 so the LDS buffer index is static.
+  __device__ __forceinline__ void mainloop(f32x4 (&acc)[8][4], int kb, int kend) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ke = kend;
+    // the previous tile's last reads / DMA of this workgroup must be done before the buffers are refilled
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stage(kb, 0);
+    stage(kb + 1, 1);
+    if (kend - kb > 1)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's 8 copies of the first tile
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    bf16x8 wx[4], wy[4], al[4], ah[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wx[i] = rd_w<0>(0, i);
+      al[i] = rd_a<0>(0, i);
+    }
+    int kt = kb;
+    for (; kt + 1 < kend; kt += 2) {
+      ktile<0>(acc, wx, wy, al, ah, kt);
+      ktile<1>(acc, wx, wy, al, ah, kt + 1);
+    }
+    if (kt < kend) ktile<0>(acc, wx, wy, al, ah, kt);
+  }
 
   // ---- epilogue: lane holds C[m][n..n+3] for m = m_base + mi*16 + (lane&15), n = n_base + ni*16 + 4*(lane>>4)
-  const int m_base = m0 + wave_m * 128 + lr;
-  const int n_base = n0 + wave_n * 64 + lk * 4;
+  __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], int m0, int n0) {
+    const int m_base = m0 + wave_m * 128 + lr;
+    const int n_base = n0 + wave_n * 64 + lk * 4;
 
-  if constexpr (EPI == EPI_SWIGLU_BF16) {
-    // pairs (ni=0 gate, ni=1 up), (ni=2 gate, ni=3 up) -> output column (n0/2 + wave_n*32 + pair*16 + 4*(lane>>4))
-    const int F = p.N >> 1;
+    if constexpr (EPI == EPI_SWIGLU_BF16) {
+      // pairs (ni=0 gate, ni=1 up), (ni=2 gate, ni=3 up) -> output column (n0/2 + wave_n*32 + pair*16 + 4*(lane>>4))
+      const int F = p.N >> 1;
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const int m = m_base + mi * 16;
-      if (m >= p.M) continue;
-      bf16_t* orow = (bf16_t*)p.out + (long)m * p.ldo;
+      for (int mi = 0; mi < 8; ++mi) {
+        const int m = m_base + mi * 16;
+        if (m >= p.M) continue;
+        bf16_t* orow = (bf16_t*)p.out + (long)m * p.ldo;
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const int oc = (n0 >> 1) + wave_n * 32 + pr * 16 + lk * 4;
-        if (oc >= F) continue;
-        const f32x4 g = acc[mi][2 * pr];
-        const f32x4 u = acc[mi][2 * pr + 1];
-        u32x2 v;
-        v.x = pack2bf(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
-        v.y = pack2bf(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
-        *(u32x2*)(orow + oc) = v;
-      }
-    }
-    return;
-  } else {
-    float bias[4][4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n_base + ni * 16 + r;
-        bias[ni][r] = (p.bias != nullptr && n < p.N) ? bf2f(p.bias[n]) : 0.f;
-      }
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const int m = m_base + mi * 16;
-      if (m >= p.M) continue;
-      const long om = p.out_seg > 0 ? (m / p.out_seg) * p.out_seg_stride + p.out_seg_off + (m % p.out_seg) : m;
-      const float* grow = nullptr;
-      if constexpr (EPI == EPI_RESID_F32) {
-        if (p.gate != nullptr) grow = p.gate + (long)(m / p.rows_per_seg) * p.gate_seg_stride;
-      }
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int n = n_base + ni * 16;
-        if (n >= p.N) continue;
-        f32x4 v = acc[mi][ni];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += bias[ni][r];
-        if (p.act == 1) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
+        for (int pr = 0; pr < 2; ++pr) {
+          const int oc = (n0 >> 1) + wave_n * 32 + pr * 16 + lk * 4;
+          if (oc >= F) continue;
+          const f32x4 g = acc[mi][2 * pr];
+          const f32x4 u = acc[mi][2 * pr + 1];
+          u32x2 v;
+          v.x = pack2bf(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
+          v.y = pack2bf(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
+          *(u32x2*)(orow + oc) = v;
         }
-        if constexpr (EPI == EPI_STORE_BF16) {
-          bf16_t* o = (bf16_t*)p.out + om * p.ldo + n;
-          if (p.resid != nullptr) {  // ResnetBlock2D / attention residual (x + h), same layout as out
-            const bf16_t* rr = p.resid + om * p.ldo + n;
+      }
+      return;
+    } else {
+      float bias[4][4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) v[r] += bf2f(rr[r]);
-          }
-          if (n + 3 < p.N) {
-            u32x2 w;
-            w.x = pack2bf(v[0], v[1]);
-            w.y = pack2bf(v[2], v[3]);
-            *(u32x2*)o = w;
-          } else {
-            for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = f2bf(v[r]);
-          }
-        } else if constexpr (EPI == EPI_STORE_F32) {
-          float* o = (float*)p.out + om * p.ldo + n;
-          if (n + 3 < p.N) {
-            *(f32x4*)o = v;
-          } else {
-            for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = v[r];
-          }
-        } else if constexpr (EPI == EPI_RESID_F32) {
-          float* o = (float*)p.out + om * p.ldo + n;
-          f32x4 x = *(f32x4*)o;
-          if (grow != nullptr) {
-            const f32x4 g = *(const f32x4*)(grow + n);
+      for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) x[r] += v[r] * g[r];
-          } else {
+        for (int r = 0; r < 4; ++r) {
+          const int n = n_base + ni * 16 + r;
+          bias[ni][r] = (p.bias != nullptr && n < p.N) ? bf2f(p.bias[n]) : 0.f;
+        }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) x[r] += v[r];
+      for (int mi = 0; mi < 8; ++mi) {
+        const int m = m_base + mi * 16;
+        if (m >= p.M) continue;
+        const long om = p.out_seg > 0 ? (m / p.out_seg) * p.out_seg_stride + p.out_seg_off + (m % p.out_seg) : m;
+        const float* grow = nullptr;
+        if constexpr (EPI == EPI_RESID_F32) {
+          if (p.gate != nullptr) grow = p.gate + (long)(m / p.rows_per_seg) * p.gate_seg_stride;
+        }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int n = n_base + ni * 16;
+          if (n >= p.N) continue;
+          f32x4 v = acc[mi][ni];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += bias[ni][r];
+          if (p.act == 1) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
           }
-          *(f32x4*)o = x;
+          if constexpr (EPI == EPI_STORE_BF16) {
+            bf16_t* o = (bf16_t*)p.out + om * p.ldo + n;
+            if (p.resid != nullptr) {  // ResnetBlock2D / attention residual (x + h), same layout as out
+              const bf16_t* rr = p.resid + om * p.ldo + n;
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (n + r < p.N) v[r] += bf2f(rr[r]);
+            }
+            if (n + 3 < p.N) {
+              u32x2 w;
+              w.x = pack2bf(v[0], v[1]);
+              w.y = pack2bf(v[2], v[3]);
+              *(u32x2*)o = w;
+            } else {
+              for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = f2bf(v[r]);
+            }
+          } else if constexpr (EPI == EPI_STORE_F32) {
+            float* o = (float*)p.out + om * p.ldo + n;
+            if (n + 3 < p.N) {
+              *(f32x4*)o = v;
+            } else {
+              for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = v[r];
+            }
+          } else if constexpr (EPI == EPI_RESID_F32) {
+            float* o = (float*)p.out + om * p.ldo + n;
+            f32x4 x = *(f32x4*)o;
+            if (grow != nullptr) {
+              const f32x4 g = *(const f32x4*)(grow + n);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) x[r] += v[r] * g[r];
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) x[r] += v[r];
+            }
+            *(f32x4*)o = x;
+          }
         }
       }
     }
   }
+};
+
+// blockIdx -> XCD-contiguous index (bijective; the dispatcher places block b on XCD b % 8)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// linear tile id -> (m0, n0): groups of 8 M-tiles, M-fastest inside a group (L2 reuse of W columns)
+__device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0, int& n0) {
+  constexpr int GROUP = 8;
+  const int group_size = GROUP * num_n;
+  const int gid = L / group_size;
+  const int first_m = gid * GROUP;
+  const int gm = min(num_m - first_m, GROUP);
+  const int rem = L - gid * group_size;
+  m0 = (first_m + rem % gm) * BM;
+  n0 = (rem / gm) * BN;
+}
+
+__device__ __forceinline__ long sk_start(int g, long I, int G) { return (long)g * I / G; }
+
+// Diagnostic build only (f-lite_amd/tools/sk_probe.hip): per-workgroup s_memrealtime stamps of the stream-K
+// phases into p.sk_stamps[wg * 8 + i].
+#ifdef FLITE_SK_STAMPS
+#define SK_STAMP(i)                                                                                   \
+  do {                                                                                                \
+    if (c.tid == 0 && p.sk_stamps) p.sk_stamps[wg * 8 + (i)] = __builtin_amdgcn_s_memrealtime();     \
+  } while (0)
+#else
+#define SK_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
+// Stream-K + data-parallel (persistent grid G = one workgroup per CU). Tiles [0, sk_tiles) are cut into
+// G contiguous, equal ranges of k-tile iterations (I / G < nk, so a range touches at most 2 tiles); the
+// remaining tiles are data parallel. A range's segment that ends inside its tile is a PARTIAL: written to
+// workspace slot wg (fp32, lane-linear) and published with a flag. The segment that ends a tile FINISHES
+// it: adds the partials of the lower-index workgroups that own the tile's earlier segments, in a fixed
+// order, then runs the epilogue. Order per workgroup: data-parallel tiles, partial, finisher -- producers
+// publish before any wait, so every wait is on work that never waits (no cycle).
+template <int EPI>
+__device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&acc)[8][4], int num_m, int num_n,
+                                              int nk, int wg) {
+  const GemmParams& p = c.p;
+  int m0, n0;
+  const int G = gridDim.x;
+  const int T = num_m * num_n;
+  const long I = (long)p.sk_tiles * nk;
+  const long it0 = sk_start(wg, I, G), it1 = sk_start(wg + 1, I, G);
+  const int jf = (int)(it0 / nk);            // tile of the first segment
+  const int jl = (int)((it1 - 1) / nk);      // tile of the last segment
+  const bool has_range = it1 > it0;
+  f32x4* slab = (f32x4*)p.sk_ws;
+  SK_STAMP(0);
+
+  // (1) data-parallel tiles: every workgroup in step, so the XCD-local tile block shares A/W k-slices in L2
+  for (int L = p.sk_tiles + wg; L < T; L += G) {
+    tile_origin(L, num_m, num_n, m0, n0);
+    c.setup_tile(m0, n0);
+    c.mainloop(acc, 0, nk);
+    c.epilogue(acc, m0, n0);
+  }
+  SK_STAMP(1);
+  // (2) partial: the last segment when it does not reach its tile's end
+  if (has_range) {
+    const long t0 = (long)jl * nk;
+    const int kb = (int)(max(it0, t0) - t0), kend = (int)(it1 - t0);
+    if (kend < nk) {
+      tile_origin(jl, num_m, num_n, m0, n0);
+      c.setup_tile(m0, n0);
+      c.mainloop(acc, kb, kend);
+      // publish (MI355X guide §6 G16, R1): write-through (sc1) payload stores drained by every wave, then
+      // one relaxed agent-scope flag store -- no release fence (it would write back the XCD's whole L2)
+      const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(slab + (size_t)wg * (BM * BN / 4)), (short)0, BM * BN * 4, 0x00020000);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[mi][ni]), srs,
+                                                 ((mi * 4 + ni) * NT + c.tid) * 16, 0, 16 /* sc1 */);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (c.tid == 0) __hip_atomic_store(p.sk_flags + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  SK_STAMP(2);
+  // (3) finisher: the first segment when it reaches its tile's end
+  if (has_range) {
+    const long t0 = (long)jf * nk;
+    const int kb = (int)(it0 - t0), kend = (int)(min(it1, t0 + nk) - t0);
+    if (kend == nk) {
+      tile_origin(jf, num_m, num_n, m0, n0);
+      c.setup_tile(m0, n0);
+      c.mainloop(acc, kb, kend);
+      SK_STAMP(3);
+      if (kb > 0) {
+        // producers: workgroups h < wg whose range ends inside this tile
+        int h_lo = wg;
+        while (h_lo > 0 && sk_start(h_lo, I, G) > t0) --h_lo;
+        if (c.tid == 0) {
+          for (int h = h_lo; h < wg; ++h) {
+            if (sk_start(h + 1, I, G) == sk_start(h, I, G)) continue;  // empty range: no partial
+            long spins = 0;
+            while (__hip_atomic_load(p.sk_flags + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+              __builtin_amdgcn_s_sleep(2);
+              if (++spins > (1L << 28)) __builtin_trap();  // never expected: all G workgroups are resident
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        SK_STAMP(4);
+        __syncthreads();
+        for (int h = h_lo; h < wg; ++h) {
+          if (sk_start(h + 1, I, G) == sk_start(h, I, G)) continue;
+          const f32x4* src = slab + (size_t)h * (BM * BN / 4);
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) acc[mi][ni] += src[(mi * 4 + ni) * NT + c.tid];
+        }
+        __syncthreads();
+        if (c.tid == 0)
+          for (int h = h_lo; h < wg; ++h) __hip_atomic_store(p.sk_flags + h, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      c.epilogue(acc, m0, n0);
+    }
+  }
+  SK_STAMP(5);
+#ifdef FLITE_SK_STAMPS
+  if (c.tid == 0 && p.sk_stamps) {
+    p.sk_stamps[wg * 8 + 6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    p.sk_stamps[wg * 8 + 7] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+  }
+#endif
+}
+
+int g_num_cu = 0;
+
+// Stream-K split for a workspace-carrying launch, in units of one k-tile iteration of one workgroup:
+//   data parallel  ceil(T / G) * nk
+//   stream-K       floor(T / G) * nk + 1.1 * (T % G) * nk / G + 24
+// The 1.1 and 24 (partial-slab write/read, two extra pipeline prologues, finisher epilogue) are fitted to
+// tools/sk_probe.py timelines on MI355X: at M = 8224, N = 3072 stream-K wins at K = 12288 (-11 %) and loses
+// at K = 3072 (+6 %), so it is taken only with a 3 % margin.
+int choose_sk_tiles(const GemmParams& p, int T) {
+  if (p.sk_ws == nullptr || p.sk_flags == nullptr || g_num_cu <= 0) return 0;
+  const int G = g_num_cu;
+  const int rem = T % G;
+  if (rem == 0) return 0;
+  const double nk = p.K / BK;
+  if (rem * nk < 2.0 * G) return 0;  // ranges of at least 2 k-tiles
+  const double dp = (double)(T / G + 1) * nk;
+  const double sk = (double)(T / G) * nk + 1.1 * rem * nk / G + 24.0;
+  return sk < 0.97 * dp ? rem : 0;
 }
 
 template <int EPI>
-int launch(const GemmParams& p, hipStream_t s) {
+int launch(GemmParams p, hipStream_t s) {
   const int num_m = (p.M + BM - 1) / BM;
   const int num_n = (p.N + BN - 1) / BN;
-  const int grid = num_m * num_n;
+  const int T = num_m * num_n;
+  p.sk_tiles = choose_sk_tiles(p, T);
+  const int grid = p.sk_tiles ? g_num_cu : T;
   if (p.conv_in != nullptr)
     hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true>), dim3(grid), dim3(NT), LDS_BYTES, s, p);
   else
@@ -443,8 +598,29 @@ int gemm_init() {
   FLITE_HIP_CHECK(set_attrs<EPI_STORE_F32>());
   FLITE_HIP_CHECK(set_attrs<EPI_RESID_F32>());
   FLITE_HIP_CHECK(set_attrs<EPI_SWIGLU_BF16>());
+  {
+    int dev = 0;
+    FLITE_HIP_CHECK(hipGetDevice(&dev));
+    hipDeviceProp_t prop;
+    FLITE_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+    g_num_cu = prop.multiProcessorCount;
+    int per_cu = 0;  // the stream-K grid needs every workgroup resident at once
+    FLITE_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_bf16_kernel<EPI_RESID_F32, false>, NT,
+                                                                LDS_BYTES));
+    if (per_cu < 1) g_num_cu = 0;
+  }
   attrs_done = true;
   return 0;
+}
+
+int gemm_sk_workspace_cus() {
+  if (gemm_init()) return 0;
+  return g_num_cu;
+}
+
+size_t gemm_sk_workspace_bytes() {
+  const int G = gemm_sk_workspace_cus();
+  return (size_t)G * BM * BN * sizeof(float) + (size_t)G * sizeof(int);
 }
 
 int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {

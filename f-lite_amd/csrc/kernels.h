@@ -33,7 +33,17 @@ struct GemmParams {
   const bf16_t* conv_in = nullptr;
   long conv_in_bytes = 0;
   int conv_ih = 0, conv_iw = 0, conv_c = 0, conv_oh = 0, conv_ow = 0, conv_up = 0;
+  // stream-K workspace (optional): fp32 partial tiles [CUs][256*256] + int flags [CUs], zero-initialised.
+  // When present the launcher may cut a partial last wave of tiles into equal k-ranges (gemm.hip).
+  float* sk_ws = nullptr;
+  int* sk_flags = nullptr;
+  int sk_tiles = 0;  // set by the launcher
+  unsigned long long* sk_stamps = nullptr;  // diagnostic build only (FLITE_SK_STAMPS)
 };
+
+// bytes of the stream-K workspace (partials + flags) for the current device
+size_t gemm_sk_workspace_bytes();
+int gemm_sk_workspace_cus();
 
 int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream);
 

@@ -53,6 +53,8 @@ SIGNATURES = {
     "flite_last_error": (_cp, []),
     "flite_version": (_i, []),
     "flite_gemm_bf16": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _vp, _i, _vp, _l, _vp, _l, _i]),
+    "flite_gemm_workspace_bytes": (_l, []),
+    "flite_gemm_bf16_ws": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _vp, _i, _vp, _l, _vp, _l, _i, _vp]),
     "flite_attn_varlen_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _f, _f]),
     "flite_rmsnorm_modulate": (_i, [_vp, _vp, _i, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_rope_qknorm": (_i, [_vp, _vp, _l, _l, _i, _i, _vp, _vp, _l, _f]),
@@ -143,9 +145,16 @@ def _ptr(t):
 # ------------------------------------------------------------------------------------------------
 # kernel-level operators
 # ------------------------------------------------------------------------------------------------
+def gemm_workspace(device) -> torch.Tensor:
+    """Zero-filled stream-K workspace for gemm(..., workspace=) on `device` (flite_gemm_workspace_bytes)."""
+    n = int(load().flite_gemm_workspace_bytes())
+    return torch.zeros(max(n, 16), dtype=torch.uint8, device=device)
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, *, out=None, epilogue=EPI_STORE_BF16, w2=None,
-         gate=None, gate_seg_stride=0, rows_per_seg=1) -> torch.Tensor:
-    """C = a . w^T (+bias) with the selected fused epilogue. a:[M,K] bf16, w:[N,K] bf16 (nn.Linear layout)."""
+         gate=None, gate_seg_stride=0, rows_per_seg=1, workspace=None) -> torch.Tensor:
+    """C = a . w^T (+bias) with the selected fused epilogue. a:[M,K] bf16, w:[N,K] bf16 (nn.Linear layout).
+    `workspace` (gemm_workspace) enables the stream-K split of a partial last wave of tiles."""
     lib = load()
     M, K = a.shape
     N = w.shape[0]
@@ -167,11 +176,13 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, *, out=None, epilogue=EPI_
     require_gpu(out, "out", contiguous=False)
     if bias is not None:
         require_gpu(bias, "bias", torch.bfloat16)
-    st = lib.flite_gemm_bf16(
-        stream_ptr(a.device), M, Nv, K, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), _ptr(w2),
-        _ptr(bias), epilogue, out.data_ptr(), out.stride(0), _ptr(gate), gate_seg_stride, rows_per_seg,
-    )
-    check(st, "flite_gemm_bf16")
+    args = (stream_ptr(a.device), M, Nv, K, a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0), _ptr(w2),
+            _ptr(bias), epilogue, out.data_ptr(), out.stride(0), _ptr(gate), gate_seg_stride, rows_per_seg)
+    if workspace is not None:
+        require_gpu(workspace, "workspace", contiguous=True)
+        check(lib.flite_gemm_bf16_ws(*args, workspace.data_ptr()), "flite_gemm_bf16_ws")
+    else:
+        check(lib.flite_gemm_bf16(*args), "flite_gemm_bf16")
     return out
 
 

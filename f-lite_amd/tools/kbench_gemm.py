@@ -48,30 +48,43 @@ def check_resid(M, N, K, T):
     err = (x - ref).norm() / ref.norm()
     print(f"resid M={M} N={N} K={K} T={T}: rel_l2={err.item():.3e}", flush=True)
 
-def bench(M, N, K, iters=20, epi=nat.EPI_STORE_BF16):
+WS = None
+
+
+def bench(M, N, K, iters=20, epi=nat.EPI_STORE_BF16, rounds=5):
+    """DP (no workspace) vs stream-K (workspace) interleaved in one process; median ms per launch."""
+    global WS
+    if WS is None:
+        WS = nat.gemm_workspace(dev)
     a = torch.randn(M, K, device=dev).bfloat16()
     w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
     w2 = (torch.randn(N, K, device=dev) * 0.05).bfloat16() if epi == nat.EPI_SWIGLU_BF16 else None
     out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    for _ in range(3):
-        nat.gemm(a, w, out=out, epilogue=epi, w2=w2)
-    torch.cuda.synchronize()
     s = torch.cuda.Event(enable_timing=True); e = torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        nat.gemm(a, w, out=out, epilogue=epi, w2=w2)
-    e.record(); torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / iters
+    res = {"dp": [], "sk": []}
+    for _ in range(rounds):
+        for mode in ("dp", "sk"):
+            ws = WS if mode == "sk" else None
+            for _ in range(2):
+                nat.gemm(a, w, out=out, epilogue=epi, w2=w2, workspace=ws)
+            torch.cuda.synchronize()
+            s.record()
+            for _ in range(iters):
+                nat.gemm(a, w, out=out, epilogue=epi, w2=w2, workspace=ws)
+            e.record(); torch.cuda.synchronize()
+            res[mode].append(s.elapsed_time(e) / iters)
     Nf = 2 * N if epi == nat.EPI_SWIGLU_BF16 else N
-    tf = 2 * M * Nf * K / ms / 1e9
-    # torch (hipBLASLt) reference speed
+    fl = 2 * M * Nf * K
+    med = {k: sorted(v)[len(v) // 2] for k, v in res.items()}
     wt = torch.randn(Nf, K, device=dev).bfloat16()
     for _ in range(3): torch.mm(a, wt.t())
     torch.cuda.synchronize(); s.record()
     for _ in range(iters): torch.mm(a, wt.t())
     e.record(); torch.cuda.synchronize()
     ms_t = s.elapsed_time(e) / iters
-    print(f"bench M={M} N={Nf} K={K} epi={epi}: {ms:.3f} ms {tf:.0f} TF/s | torch.mm {ms_t:.3f} ms {2*M*Nf*K/ms_t/1e9:.0f} TF/s", flush=True)
+    print(f"bench M={M} N={Nf} K={K} epi={epi}: dp {med['dp']:.3f} ms {fl/med['dp']/1e9:.0f} TF/s | "
+          f"sk {med['sk']:.3f} ms {fl/med['sk']/1e9:.0f} TF/s | torch.mm {ms_t:.3f} ms {fl/ms_t/1e9:.0f} TF/s",
+          flush=True)
 
 if __name__ == "__main__":
     check(256, 256, 64)
@@ -85,3 +98,4 @@ if __name__ == "__main__":
     bench(8224, 12288, 3072, epi=nat.EPI_SWIGLU_BF16)
     bench(8224, 3072, 12288)
     bench(8192, 8192, 8192, iters=10)
+    bench(8224, 1536, 3072, epi=nat.EPI_SWIGLU_BF16)

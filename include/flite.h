@@ -45,6 +45,23 @@ int flite_gemm_bf16(void* stream, int M, int N, int K, const void* A, long lda, 
                     long gate_seg_stride, int rows_per_seg);
 
 /*
+ * Bytes of the optional stream-K workspace of flite_gemm_bf16_ws on the current device (fp32 partial tiles
+ * + flags, one slot per CU).
+ */
+long flite_gemm_workspace_bytes(void);
+
+/*
+ * flite_gemm_bf16 with a caller-owned stream-K workspace (device memory of flite_gemm_workspace_bytes(),
+ * zero-filled once before first use; every launch leaves it zeroed). When the last wave of 256x256 output
+ * tiles is partial, the launch runs one workgroup per CU and splits that wave's k-iterations evenly over
+ * them (partials reduced in a fixed order: deterministic). Launches sharing a workspace must be
+ * stream-ordered.
+ */
+int flite_gemm_bf16_ws(void* stream, int M, int N, int K, const void* A, long lda, const void* W, long ldw,
+                       const void* W2, const void* bias, int epilogue, void* out, long ldo, const float* gate,
+                       long gate_seg_stride, int rows_per_seg, void* workspace);
+
+/*
  * Varlen flash-attention forward, head_dim 256, non-causal.
  * Replaces flash_attn_interface.flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
  * max_seqlen_k, softmax_scale) (f_lite/model.py:203-210). Token t of sequence b is row cu[b]+t; head h of

@@ -84,6 +84,52 @@ def test_gemm_gated_residual(shared):
     assert rel(x, ref) < 1e-5
 
 
+# Stream-K (flite_gemm_bf16_ws): shapes whose last wave of 256x256 tiles is partial on 256 CUs and whose k-depth
+# makes the split pay (gemm.hip choose_sk_tiles), so the launcher cuts that wave's k-iterations evenly over the
+# CUs: the 10B down projection, and small grids where one tile is shared by up to ~28 workgroups (fan-in).
+@pytest.mark.parametrize("M,N,K", [(8224, 3072, 12288), (2000, 2304, 8192), (1000, 768, 16384), (600, 520, 4096)])
+def test_gemm_stream_k(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(K)
+    a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) * 0.05).bfloat16()
+    b = (torch.randn(N, device=DEV, generator=g) * 0.1).bfloat16()
+    ws = nat.gemm_workspace(DEV)
+    ref = a.double() @ w.double().t() + b.double()
+    # fp32 store: rel-L2 vs fp64 at fp32-accumulation level, same as the data-parallel path
+    dp = nat.gemm(a, w, b, epilogue=nat.EPI_STORE_F32)
+    sk = nat.gemm(a, w, b, epilogue=nat.EPI_STORE_F32, workspace=ws)
+    assert rel(sk, ref) < 1e-5 and rel(dp, ref) < 1e-5
+    assert not torch.equal(sk, dp)  # the split path ran (different fp32 summation order)
+    # deterministic: the same split and reduction order on every launch (flags reset by the finishers)
+    sk2 = nat.gemm(a, w, b, epilogue=nat.EPI_STORE_F32, workspace=ws)
+    assert torch.equal(sk, sk2)
+    n_cu = ws.numel() // (256 * 256 * 4 + 4)
+    assert int(ws[n_cu * 256 * 256 * 4:].view(torch.int32).abs().sum().item()) == 0  # every flag back to 0
+    # gated residual (the engine's proj / down GEMMs)
+    T = M // 2 if M % 2 == 0 else M
+    gate = torch.randn((M + T - 1) // T, N, device=DEV)
+    x0 = torch.randn(M, N, device=DEV)
+    x = x0.clone()
+    nat.gemm(a, w, b, out=x, epilogue=nat.EPI_RESID_F32, gate=gate, gate_seg_stride=N, rows_per_seg=T,
+             workspace=ws)
+    y = a.float() @ w.float().t() + b.float()
+    refx = x0 + y * gate.repeat_interleave(T, dim=0)[:M]
+    assert rel(x, refx) < 1e-5
+    # bf16 store
+    out = nat.gemm(a, w, b, workspace=ws)
+    assert rel(out, ref) < 1e-2
+
+
+def test_gemm_stream_k_swiglu():
+    M, F, K = 2000, 1152, 8192  # N = 2F = 2304: 72 tiles, stream-K
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    wg = (torch.randn(F, K, device=DEV) * 0.05).bfloat16()
+    wu = (torch.randn(F, K, device=DEV) * 0.05).bfloat16()
+    ref = torch.nn.functional.silu(a.float() @ wg.float().t()) * (a.float() @ wu.float().t())
+    out = nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu, workspace=nat.gemm_workspace(DEV))
+    assert rel(out, ref) < 1e-2
+
+
 def _attn_ref(q, k, v, cu_q, cu_k, scale):
     return R.attention_varlen(q.float().cpu(), k.float().cpu(), v.float().cpu(), cu_q.cpu(), cu_k.cpu(), scale)
 
