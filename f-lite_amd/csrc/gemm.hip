@@ -545,6 +545,30 @@ __device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&ac
 #endif
 }
 
+// One launch: data-parallel (grid = tiles, one output tile per workgroup) or, when the launcher set
+// p.sk_tiles, the persistent stream-K + data-parallel schedule above (grid = one workgroup per CU).
+template <int EPI, bool CONV>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  GemmCta<EPI, CONV> c(p, smem);
+  const int num_m = (p.M + BM - 1) / BM;
+  const int num_n = (p.N + BN - 1) / BN;
+  const int nk = p.K / BK;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  f32x4 acc[8][4];
+  if constexpr (!CONV) {
+    if (p.sk_tiles > 0) {
+      stream_k_body<EPI>(c, acc, num_m, num_n, nk, wg);
+      return;
+    }
+  }
+  int m0, n0;
+  tile_origin(wg, num_m, num_n, m0, n0);
+  c.setup_tile(m0, n0);
+  c.mainloop(acc, 0, nk);
+  c.epilogue(acc, m0, n0);
+}
+
 int g_num_cu = 0;
 
 // Stream-K split for a workspace-carrying launch, in units of one k-tile iteration of one workgroup:
