@@ -224,15 +224,25 @@ def main():
                 tr = json.loads(pmc.read_text()).get(args.probe)
                 if tr:
                     roofline["traffic"] = tr["hbm_bytes_per_launch"]
+                    roofline["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes over "
+                                                  "f-lite_amd/tools/pmc_gemm.py (same kernel and shape), "
+                                                  "profiles/pmc_traffic.json; L2->fabric bytes incl. "
+                                                  "Infinity-Cache hits")
+                    roofline["algorithmic_bytes_per_launch"] = 2.0 * (M * D + 2 * F * D + M * F)
+                    if "mfma_busy_frac" in tr:
+                        roofline["pmc_mfma_busy_frac"] = round(tr["mfma_busy_frac"], 4)
             except Exception:
                 pass
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline_sample(model, cfg, args.height, args.width, args.sample_steps)
 
+    metric = "images/sec @%dx%d, %d steps, F-Lite-%s bf16" % (args.height, args.width, args.sample_steps,
+                                                              args.model.upper())
+    if (args.model, args.height, args.width, args.sample_steps) == ("10b", 1024, 1024, 30):
+        metric += "; 1/8 GPU + MFMA util%"  # BASELINE.json's metric string (util in mfma_util_image)
     line = {
-        "metric": "images/sec @%dx%d, %d steps, F-Lite-%s bf16" % (args.height, args.width, args.sample_steps,
-                                                                   args.model.upper()),
+        "metric": metric,
         "value": round(value, 5),
         "unit": "images/s",
         "n_gpus": world,
