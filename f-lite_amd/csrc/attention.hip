@@ -13,6 +13,17 @@
 // K/V tiles stream HBM->LDS with buffer_load ... lds (swizzle on the source address; keys past the sequence
 // end read as zeros through the buffer range check), double-buffered; the loop is unrolled over the two
 // buffers so every LDS address is a per-lane base + an immediate offset.
+//
+// Schedule. A 4112-token sequence is 32 full 128-row q-tiles plus a 16-row tail; at B = 2, H = 12 that is
+// 768 full tiles (exactly 3 per CU on 256 CUs) and 24 tails, and every tile, full or tail, sweeps all keys.
+// One workgroup per tile runs the 24 tails as a 4th round on 24 CUs (a 25 % loss). With the bounded softmax
+// (fixed shift, so partial sums add without rescaling) and a caller workspace, the tail of each (sequence,
+// head) is instead cut into n_split contiguous ranges of key tiles ("phase B" workgroups, queued after the
+// full tiles, one short round). Each writes its unnormalised O and row sums to its own slab (write-through
+// stores) and bumps the pair's counter; the last arriver adds the slabs in slab order (deterministic: the
+// same sum on every launch), normalises and stores the rows, and resets the counter for the next launch.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -29,6 +40,13 @@ constexpr int TILE = KT * HD * 2;  // 32 KiB: one K or V tile
 constexpr int K_OFF = 0;
 constexpr int V_OFF = 2 * TILE;
 constexpr int LDS_BYTES = 4 * TILE;  // 128 KiB
+// split slab: O^T accumulators lane-linear [wave 4][i 8][r4 4][lane 64] f32x4, then l [wave 4][lane 64]
+constexpr int SLAB_O_FLOATS = 4 * 8 * 4 * 64 * 4;
+constexpr int SLAB_FLOATS = SLAB_O_FLOATS + 4 * 64;
+constexpr long SLAB_BYTES = (long)SLAB_FLOATS * 4;
+constexpr long CNT_BYTES = 4096;  // counter block at the workspace start (1024 (sequence, head) pairs)
+constexpr int MAX_SPLIT = 16;     // key ranges per tail
+constexpr int MIN_SPLIT_KEYS = 16 * KT;  // shorter key ranges: the tail round is cheaper than the hand-off
 
 __device__ __forceinline__ s16x4 ds_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(p));
@@ -68,6 +86,25 @@ __device__ __forceinline__ unsigned lds_addr_of(const void* p) {
   return (unsigned)(unsigned long long)(const LDS_AS char*)p;
 }
 
+// blockIdx -> XCD-contiguous index (bijective; the dispatcher deals blocks round-robin over the 8 XCDs)
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int xcd = bid & 7, q8 = n >> 3, r8 = n & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+// Diagnostic build only (f-lite_amd/tools/attn_probe.hip): per-workgroup s_memrealtime stamps into
+// p.stamps[blockIdx.x * 4 + i]: 0 start, 1 main loop done, 2 end, 3 XCC id << 32 | HW_ID.
+#ifdef FLITE_ATTN_STAMPS
+#define ATTN_STAMP(i)                                                                                  \
+  do {                                                                                                 \
+    if (tid == 0 && p.stamps) p.stamps[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();       \
+  } while (0)
+#else
+#define ATTN_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 // BOUNDED: every score s*scale is known to lie in [-max_score, max_score] (QK-normed q and k: |q|,|k| <= 16
 // for head_dim 256, so |q.k|/16 <= 16 -- model.py:180,197 precede every attention call of the DiT). Softmax is
 // shift-invariant, so the running max is replaced by the fixed bound: no row max, no O/l rescale, p <= 1.
@@ -76,38 +113,60 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
-  // XCD-aware mapping of the 1-D grid: workgroups are dealt round-robin over the 8 XCDs (bid % 8), so the
-  // bijective remap gives each XCD a contiguous range of (sequence, head, q-tile) work in which consecutive
-  // workgroups share one (sequence, head) and its K/V stream.
-  int b, h, qt;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  ATTN_STAMP(0);
+#ifdef FLITE_ATTN_STAMPS
+  if (tid == 0 && p.stamps)
+    p.stamps[blockIdx.x * 4 + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                   (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
+  // Work decode. Phase A (blocks [0, nA)): one 128-row q-tile of one (sequence, head), all keys. Phase B
+  // (the rest): key range `chunk` of the tail rows [n_main*QT, q_len) of one (sequence, head).
+  // Each phase is remapped XCD-aware, so consecutive workgroups of one XCD share a (sequence, head) and its
+  // K/V stream in L2.
+  int b, h, q0, chunk = -1;
   {
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    qt = v % p.n_qtiles;
-    const int pair = v / p.n_qtiles;
+    const int nA = p.B * p.H * p.n_main;
+    const bool phase_a = (int)blockIdx.x < nA;
+    const int v = phase_a ? xcd_remap(blockIdx.x, nA) : xcd_remap(blockIdx.x - nA, gridDim.x - nA);
+    int pair;
+    if (phase_a) {
+      q0 = (v % p.n_main) * QT;
+      pair = v / p.n_main;
+    } else {
+      chunk = v % p.n_split;
+      pair = v / p.n_split;
+      q0 = p.n_main * QT;
+    }
     h = pair % p.H;
     b = pair / p.H;
   }
 
   const int q_start = p.cu_q[b];
   const int q_len = p.cu_q[b + 1] - q_start;
-  if (qt * QT >= q_len) return;  // uniform over the workgroup
+  if (q0 >= q_len) return;  // uniform over the workgroup (and over all chunks of a pair)
   const int k_start = p.cu_k[b];
   const int k_len = p.cu_k[b + 1] - k_start;
 
   const int lq = lane & 31;
   const int hh = lane >> 5;
-  const int q_row = qt * QT + wave * 32 + lq;  // this lane's query (within the sequence)
+  const int q_row = q0 + wave * 32 + lq;  // this lane's query (within the sequence)
 
-  if (k_len <= 0) {  // no keys: output zeros
-    if (q_row < q_len) {
+  if (k_len <= 0) {  // no keys: output zeros (one chunk writes them)
+    if (chunk <= 0 && q_row < q_len) {
       bf16_t* o = p.o + (long)(q_start + q_row) * p.o_row_stride + (long)h * p.o_head_stride;
       for (int d = hh * 128; d < hh * 128 + 128; d += 4) *(u32x2*)(o + d) = u32x2{0u, 0u};
     }
     return;
   }
+  const int ntiles_all = (k_len + KT - 1) / KT;
+  int t_begin = 0, t_end = ntiles_all;
+  if (chunk >= 0) {
+    const int per = (ntiles_all + p.n_split - 1) / p.n_split;
+    t_begin = min(chunk * per, ntiles_all);
+    t_end = min(t_begin + per, ntiles_all);
+  }
+  const int nt = t_end - t_begin;
 
   // ---- Q^T fragments (B operand): lane holds Q[q][16s + 8*hh + j], s = 0..15 ----
   bf16x8 qf[16];
@@ -119,33 +178,32 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
   }
 
   // ---- staging: 8 K + 8 V LDS-DMA pieces per wave per tile; piece qi covers tile rows 2qi, 2qi+1.
-  // Keys >= k_len get an out-of-range offset -> the buffer range check returns zeros.
-  const i32x4 krs = make_rsrc(p.k + (long)k_start * p.k_row_stride + (long)h * p.k_head_stride, 0x7fffffffu);
-  const i32x4 vrs = make_rsrc(p.v + (long)k_start * p.v_row_stride + (long)h * p.v_head_stride, 0x7fffffffu);
+  // Per-lane source offsets are tile-invariant; each tile moves the descriptor base to its first key and sets
+  // the range to the keys left in the sequence, so keys >= k_len read as zeros (buffer range check).
+  const long k_base = (long)k_start * p.k_row_stride + (long)h * p.k_head_stride;
+  const long v_base = (long)k_start * p.v_row_stride + (long)h * p.v_head_stride;
   const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr_of(smem));
-  unsigned k_src[8], v_src[8];  // byte offsets of this lane's piece elements for key row `row` (tile 0)
-  int st_row[8];
+  unsigned k_src[8], v_src[8];  // byte offsets of this lane's piece within a tile
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int row = 2 * (wave * 8 + i) + hh;
     const int pos = lane & 31;
     const int kc = pos ^ (row & 15);                              // K: 16-B chunk XOR (row & 15)
     const int vc = (((pos >> 2) ^ (row & 3)) << 2) | (pos & 3);   // V: 64-B block XOR (row & 3)
-    st_row[i] = row;
-    k_src[i] = (unsigned)(kc * 16);
-    v_src[i] = (unsigned)(vc * 16);
+    k_src[i] = (unsigned)(row * p.k_row_stride * 2 + kc * 16);
+    v_src[i] = (unsigned)(row * p.v_row_stride * 2 + vc * 16);
   }
   auto stage = [&](int t, int buf) {
+    const long rows_left = k_len - (long)t * KT;
+    const i32x4 krs = make_rsrc(p.k + k_base + (long)t * KT * p.k_row_stride,
+                                (unsigned)min(rows_left * p.k_row_stride * 2, 0x7fffffffL));
+    const i32x4 vrs = make_rsrc(p.v + v_base + (long)t * KT * p.v_row_stride,
+                                (unsigned)min(rows_left * p.v_row_stride * 2, 0x7fffffffL));
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int qi = wave * 8 + i;
-      const int key = t * KT + st_row[i];
-      const bool ok = key < k_len;
-      const unsigned ko = ok ? (unsigned)(key * p.k_row_stride * 2) + k_src[i] : 0x80000000u;
-      const unsigned vo = ok ? (unsigned)(key * p.v_row_stride * 2) + v_src[i] : 0x80000000u;
-      const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds0 + buf * TILE + qi * 1024));
-      blds16(krs, ko, dst + K_OFF);
-      blds16(vrs, vo, dst + V_OFF);
+      const unsigned dst = lds0 + buf * TILE + (wave * 8 + i) * 1024;
+      blds16(krs, k_src[i], dst + K_OFF);
+      blds16(vrs, v_src[i], dst + V_OFF);
     }
   };
 
@@ -256,26 +314,108 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     }
   };
 
-  const int ntiles = (k_len + KT - 1) / KT;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < ntiles; t += 2) {
-    if (t + 1 < ntiles) stage(t + 1, 1);
-    compute(0);
+  if (nt > 0) {
+    stage(t_begin, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t + 1 >= ntiles) break;
-    if (t + 2 < ntiles) stage(t + 2, 0);
-    compute(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    for (int j = 0; j < nt; j += 2) {
+      if (j + 1 < nt) stage(t_begin + j + 1, 1);
+      compute(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (j + 1 >= nt) break;
+      if (j + 2 < nt) stage(t_begin + j + 2, 0);
+      compute(1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
+  ATTN_STAMP(1);
   // keys past the end were staged as zero rows: each contributed exp2(0*sl2 - m) to l and 0 to O
   l_run += __shfl_xor(l_run, 32, 64);  // the two lane halves hold the sums of complementary keys
-  const int n_pad = ntiles * KT - k_len;
+  const int n_pad = nt > 0 ? max(0, t_end * KT - k_len) : 0;
   l_run -= (float)n_pad * __builtin_amdgcn_exp2f(-m_run);
+
+  if constexpr (BOUNDED) {
+    if (chunk >= 0) {
+      // ---- phase B hand-off (MI355X guide §6 G16: write-through payload, vmcnt drain, relaxed flag) ----
+      const int pair = b * p.H + h;
+      const bool live = wave * 32 < q_len - q0;  // wave-uniform: this wave has tail rows
+      char* slab0 = (char*)p.split_ws + CNT_BYTES + (size_t)pair * p.n_split * SLAB_BYTES;
+      if (live) {
+        const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(slab0 + (size_t)chunk * SLAB_BYTES), (short)0, (int)SLAB_BYTES, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const f32x4 v = {o_acc[i][4 * r4], o_acc[i][4 * r4 + 1], o_acc[i][4 * r4 + 2], o_acc[i][4 * r4 + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), srs,
+                                                   (((wave * 8 + i) * 4 + r4) * 64 + lane) * 16, 0, 16 /* sc1 */);
+          }
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(l_run), srs, SLAB_O_FLOATS * 4 + (wave * 64 + lane) * 4,
+                                              0, 16 /* sc1 */);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* cnt = (int*)p.split_ws + pair;
+      volatile LDS_AS int* flag = (volatile LDS_AS int*)lds0;  // K/V buffers are idle now
+      if (tid == 0) *flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (*flag != p.n_split - 1) {  // not the last arriver (uniform)
+        ATTN_STAMP(2);
+        return;
+      }
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // Reduce with the whole workgroup. Every slab load of an element is issued before any is consumed
+      // (addresses clamped to a valid slab, the excess masked after the load: no branch around a load), and
+      // the sum runs in slab order. Row sums first (to LDS, after the flag word), then the O elements
+      // e = t, t + 256, ... of the live waves' lane-linear slab part; rows past q_len are skipped.
+      const int n_live = min(4, (q_len - q0 + 31) / 32);
+      volatile LDS_AS float* lsum = (volatile LDS_AS float*)(lds0 + 16);
+      const int ns = p.n_split;
+      if (tid < n_live * 64) {
+        float lv[MAX_SPLIT];
+#pragma unroll
+        for (int c = 0; c < MAX_SPLIT; ++c)
+          lv[c] = ((const float*)(slab0 + (size_t)min(c, ns - 1) * SLAB_BYTES))[SLAB_O_FLOATS + tid];
+        float l = 0.f;
+#pragma unroll
+        for (int c = 0; c < MAX_SPLIT; ++c) l += c < ns ? lv[c] : 0.f;
+        lsum[tid] = l;
+      }
+      __syncthreads();
+      for (int e = tid; e < n_live * 2048; e += NT) {
+        const int w = e >> 11, ln = e & 63;
+        const int row = q0 + 32 * w + (ln & 31);
+        if (row >= q_len) continue;
+        f32x4 v[MAX_SPLIT];
+#pragma unroll
+        for (int c = 0; c < MAX_SPLIT; ++c)
+          v[c] = *(const f32x4*)((const float*)(slab0 + (size_t)min(c, ns - 1) * SLAB_BYTES) + e * 4);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < MAX_SPLIT; ++c)
+          if (c < ns) acc += v[c];
+        const float l = lsum[w * 64 + ln];
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+        const int d = ((e >> 8) & 7) * 32 + 8 * ((e >> 6) & 3) + 4 * (ln >> 5);
+        u32x2 st;
+        st.x = pack2bf(acc[0] * inv, acc[1] * inv);
+        st.y = pack2bf(acc[2] * inv, acc[3] * inv);
+        *(u32x2*)(p.o + (long)(q_start + row) * p.o_row_stride + (long)h * p.o_head_stride + d) = st;
+      }
+      ATTN_STAMP(2);
+      return;
+    }
+  }
+
   if (q_row >= q_len) return;
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
   bf16_t* orow = p.o + (long)(q_start + q_row) * p.o_row_stride + (long)h * p.o_head_stride;
@@ -290,9 +430,11 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       *(u32x2*)(orow + d) = w;
     }
   }
+  ATTN_STAMP(2);
 }
 
 bool attr_done = false;
+int g_attn_cus = 0;
 
 }  // namespace
 
@@ -302,8 +444,20 @@ int attn_init() {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
   FLITE_HIP_CHECK(hipFuncSetAttribute((const void*)attn_fwd_hd256_kernel<false>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+  int dev = 0;
+  FLITE_HIP_CHECK(hipGetDevice(&dev));
+  FLITE_HIP_CHECK(hipDeviceGetAttribute(&g_attn_cus, hipDeviceAttributeMultiprocessorCount, dev));
   attr_done = true;
   return 0;
+}
+
+long attn_split_workspace_bytes(int B, int H) {
+  if (attn_init()) return 0;
+  const int pairs = B * H;
+  if (pairs <= 0 || pairs > (int)(CNT_BYTES / 4)) return 0;
+  const int S = std::min(g_attn_cus / pairs, MAX_SPLIT);  // tail pieces fill at most one round of the chip
+  if (S < 2) return 0;
+  return CNT_BYTES + (long)pairs * S * SLAB_BYTES;
 }
 
 int attn_fwd(const AttnParams& p, hipStream_t stream) {
@@ -316,8 +470,19 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
                 "attention: head strides must be multiples of 8 elements");
   if (attn_init()) return 1;
   AttnParams q = p;
-  q.n_qtiles = (p.max_q + QT - 1) / QT;
-  dim3 grid(q.n_qtiles * p.H * p.B);
+  q.n_main = (p.max_q + QT - 1) / QT;
+  q.n_split = 0;
+  const int pairs = p.B * p.H;
+  if (p.max_score > 0.f && p.split_ws != nullptr && p.max_q % QT != 0 && pairs <= (int)(CNT_BYTES / 4) &&
+      (p.max_k <= 0 || p.max_k >= MIN_SPLIT_KEYS)) {
+    const long cap = (p.split_ws_bytes - CNT_BYTES) / SLAB_BYTES / pairs;  // slabs per pair in the workspace
+    const int S = (int)std::min<long>(std::min(g_attn_cus / pairs, MAX_SPLIT), cap);
+    if (S >= 2) {
+      q.n_main = p.max_q / QT;
+      q.n_split = S;
+    }
+  }
+  dim3 grid(pairs * (q.n_main + q.n_split));
   if (p.max_score > 0.f)
     hipLaunchKernelGGL(attn_fwd_hd256_kernel<true>, grid, dim3(NT), LDS_BYTES, stream, q);
   else

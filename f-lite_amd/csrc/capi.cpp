@@ -101,6 +101,37 @@ int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void
   return attn_fwd(a, (hipStream_t)stream);
 }
 
+long flite_attn_workspace_bytes(int batch, int num_heads) { return attn_split_workspace_bytes(batch, num_heads); }
+
+int flite_attn_varlen_fwd_ws(void* stream, const void* q, const void* k, const void* v, void* o, long q_row_stride,
+                             long k_row_stride, long v_row_stride, long o_row_stride, long head_stride,
+                             const int* cu_seqlens_q, const int* cu_seqlens_k, int batch, int num_heads, int head_dim,
+                             int max_seqlen_q, int max_seqlen_k, float softmax_scale, float max_score,
+                             void* workspace, long workspace_bytes) {
+  AttnParams a;
+  a.q = (const bf16_t*)q;
+  a.k = (const bf16_t*)k;
+  a.v = (const bf16_t*)v;
+  a.o = (bf16_t*)o;
+  a.q_row_stride = q_row_stride;
+  a.k_row_stride = k_row_stride;
+  a.v_row_stride = v_row_stride;
+  a.o_row_stride = o_row_stride;
+  a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = head_stride;
+  a.cu_q = cu_seqlens_q;
+  a.cu_k = cu_seqlens_k;
+  a.B = batch;
+  a.H = num_heads;
+  a.head_dim = head_dim;
+  a.max_q = max_seqlen_q;
+  a.scale = softmax_scale;
+  a.max_score = max_score;
+  a.max_k = max_seqlen_k;
+  a.split_ws = workspace;
+  a.split_ws_bytes = workspace != nullptr ? workspace_bytes : 0;
+  return attn_fwd(a, (hipStream_t)stream);
+}
+
 int flite_rmsnorm_modulate(void* stream, const void* x, int x_is_bf16, long ldx, void* y, long ldy, const void* w,
                            const float* shift, const float* scale, long mod_seg_stride, long seg_rows, long rows,
                            int dim, float eps) {

@@ -57,6 +57,10 @@ void DitEngine::free_ws() {
   for (void* p : allocs_) hipFree(p);
   allocs_.clear();
   ctx_kv_.clear();
+  sk_ws_ = nullptr;
+  sk_flags_ = nullptr;
+  attn_ws_ = nullptr;
+  attn_ws_bytes_ = 0;
 }
 
 // every GEMM of the engine may use the stream-K workspace (launches on the engine's streams are ordered)
@@ -189,6 +193,11 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
       FLITE_HIP_CHECK(hipMemset(sk_flags_, 0, (size_t)G * 4));
     }
   }
+  attn_ws_bytes_ = attn_split_workspace_bytes(B, H);
+  if (attn_ws_bytes_ > 0) {
+    if (alloc(&attn_ws_, (size_t)attn_ws_bytes_)) return 1;
+    FLITE_HIP_CHECK(hipMemset(attn_ws_, 0, (size_t)attn_ws_bytes_));
+  }
   if (alloc((void**)&cu_self_, (B + 1) * 4)) return 1;
   if (alloc((void**)&cu_ctx_, (B + 1) * 4)) return 1;
   if (alloc((void**)&cos_, (long)T_ * 128 * 4)) return 1;
@@ -233,6 +242,8 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
   FLITE_HIP_CHECK(hipMemcpyAsync(cu_ctx_, cu_host, (nseq + 1) * 4, hipMemcpyHostToDevice, s));
   nctx_ = n;
   nseq_ctx_ = nseq;
+  ctx_max_len_ = 0;
+  for (int i = 0; i < nseq; ++i) ctx_max_len_ = std::max(ctx_max_len_, cu_host[i + 1] - cu_host[i]);
   if (n == 0) return 0;
   // context_proj (model.py:527) -> LigerRMSNorm (model.py:528)
   GemmParams g;
@@ -440,8 +451,11 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.H = H;
     a.head_dim = HEAD_DIM;
     a.max_q = T_;
+    a.max_k = T_;
     a.scale = 1.0f / sqrtf((float)HEAD_DIM);
     a.max_score = kQKNormScoreBound;
+    a.split_ws = attn_ws_;
+    a.split_ws_bytes = attn_ws_bytes_;
     if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
     if (attn_fwd(a, s)) return 1;
     if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
@@ -485,8 +499,11 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.H = H;
     a.head_dim = HEAD_DIM;
     a.max_q = T_;
+    a.max_k = ctx_max_len_;
     a.scale = 1.0f / sqrtf((float)HEAD_DIM);
     a.max_score = kQKNormScoreBound;
+    a.split_ws = attn_ws_;
+    a.split_ws_bytes = attn_ws_bytes_;
     if (attn_fwd(a, s)) return 1;
     if (resid(obuf_, D, b.cproj_w, D, gate_ca)) return 1;
   }

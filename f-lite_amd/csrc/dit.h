@@ -73,7 +73,7 @@ class DitEngine {
   // shape
   int B_ = 0, Hl_ = 0, Wl_ = 0, T_ = 0, HW_ = 0, ntmax_ = 0, nctx_max_ = 0;
   long M_ = 0;
-  int nctx_ = 0, nseq_ctx_ = 0;
+  int nctx_ = 0, nseq_ctx_ = 0, ctx_max_len_ = 0;
   // workspace
   float* x_ = nullptr;
   bf16_t *nbuf_ = nullptr, *qkv_ = nullptr, *obuf_ = nullptr, *hbuf_ = nullptr, *patches_ = nullptr;
@@ -81,6 +81,8 @@ class DitEngine {
   float* acc_ = nullptr;  // graph-owned Euler accumulator (sample)
   float* sk_ws_ = nullptr;  // stream-K GEMM partial tiles
   int* sk_flags_ = nullptr;
+  void* attn_ws_ = nullptr;  // attention tail-split slabs + counters (attention.hip "Schedule")
+  long attn_ws_bytes_ = 0;
   int *cu_self_ = nullptr, *cu_ctx_ = nullptr;
   float *cos_ = nullptr, *sin_ = nullptr, *inv_freq_ = nullptr;
   bf16_t* ctx_p_ = nullptr;

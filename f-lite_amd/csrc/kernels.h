@@ -60,13 +60,21 @@ struct AttnParams {
   const int* cu_k = nullptr;  // device int32 [B+1]
   int B = 0, H = 0, head_dim = 0;
   int max_q = 0;              // max query length (grid size)
+  int max_k = 0;              // max key length (0 = unknown): a hint for the schedule only
   float scale = 1.f;
   // > 0: every score*scale is bounded by +-max_score (QK-normed inputs) -> fixed-shift softmax, no rescale
   float max_score = 0.f;
-  int n_qtiles = 0;  // set by the launcher
+  // optional split workspace (attention.hip "Schedule"; bounded softmax only): zero-filled once by its owner,
+  // left zeroed by every launch; launches sharing it must be stream-ordered
+  void* split_ws = nullptr;
+  long split_ws_bytes = 0;
+  int n_main = 0, n_split = 0;  // set by the launcher
+  unsigned long long* stamps = nullptr;  // diagnostic build only (FLITE_ATTN_STAMPS)
 };
 
 int attn_fwd(const AttnParams& p, hipStream_t stream);
+// bytes of a split workspace that lets a (B sequences, H heads) launch cut its tails over the chip (0: no split)
+long attn_split_workspace_bytes(int B, int H);
 
 }  // namespace flite
 

@@ -56,6 +56,9 @@ SIGNATURES = {
     "flite_gemm_workspace_bytes": (_l, []),
     "flite_gemm_bf16_ws": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _vp, _i, _vp, _l, _vp, _l, _i, _vp]),
     "flite_attn_varlen_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _f, _f]),
+    "flite_attn_workspace_bytes": (_l, [_i, _i]),
+    "flite_attn_varlen_fwd_ws": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _i, _f,
+                                      _f, _vp, _l]),
     "flite_rmsnorm_modulate": (_i, [_vp, _vp, _i, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_rope_qknorm": (_i, [_vp, _vp, _l, _l, _i, _i, _vp, _vp, _l, _f]),
     "flite_gather_rows": (_i, [_vp, _vp, _vp, _vp, _l, _i]),
@@ -186,8 +189,16 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, *, out=None, epilogue=EPI_
     return out
 
 
-def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None, max_score=0.0):
-    """flash_attn_varlen_func replacement: q [Lq, h, 256], k/v [Lk, h, 256] (row-major, any row stride)."""
+def attn_workspace(device, batch, num_heads):
+    """Zero-filled split workspace for attn_varlen(..., workspace=) (flite_attn_workspace_bytes); None when a
+    (batch, num_heads) launch gains nothing from it."""
+    n = int(load().flite_attn_workspace_bytes(batch, num_heads))
+    return torch.zeros(n, dtype=torch.uint8, device=device) if n > 0 else None
+
+
+def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None, max_score=0.0, workspace=None, max_k=0):
+    """flash_attn_varlen_func replacement: q [Lq, h, 256], k/v [Lk, h, 256] (row-major, any row stride).
+    `workspace` (attn_workspace) lets a bounded (max_score > 0) launch split its partial q-tiles by keys."""
     lib = load()
     Lq, H, D = q.shape
     if out is None:
@@ -198,10 +209,15 @@ def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None, max_score=0.0):
             raise FliteError(f"attn: {n} must be [L, h, d] with contiguous heads")
     require_gpu(cu_q, "cu_q", torch.int32)
     require_gpu(cu_k, "cu_k", torch.int32)
-    st = lib.flite_attn_varlen_fwd(stream_ptr(q.device), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(),
-                                   q.stride(0), k.stride(0), v.stride(0), out.stride(0), D, cu_q.data_ptr(),
-                                   cu_k.data_ptr(), cu_q.numel() - 1, H, D, max_q, scale, max_score)
-    check(st, "flite_attn_varlen_fwd")
+    args = (stream_ptr(q.device), q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), q.stride(0),
+            k.stride(0), v.stride(0), out.stride(0), D, cu_q.data_ptr(), cu_k.data_ptr(), cu_q.numel() - 1, H, D,
+            max_q)
+    if workspace is not None:
+        require_gpu(workspace, "workspace", contiguous=True)
+        check(lib.flite_attn_varlen_fwd_ws(*args, max_k, scale, max_score, workspace.data_ptr(), workspace.numel()),
+              "flite_attn_varlen_fwd_ws")
+    else:
+        check(lib.flite_attn_varlen_fwd(*args, scale, max_score), "flite_attn_varlen_fwd")
     return out
 
 

@@ -75,6 +75,24 @@ int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void
                           int head_dim, int max_seqlen_q, float softmax_scale, float max_score);
 
 /*
+ * Bytes of the optional split workspace of flite_attn_varlen_fwd_ws for `batch` sequences x `num_heads` heads on
+ * the current device (0: that launch shape gains nothing from it).
+ */
+long flite_attn_workspace_bytes(int batch, int num_heads);
+
+/*
+ * flite_attn_varlen_fwd with a caller-owned split workspace (device memory, zero-filled once, left zeroed by
+ * every launch; launches sharing it must be stream-ordered). With max_score > 0 the partial last q-tile of each
+ * (sequence, head) is cut over the chip by key ranges and reduced in a fixed order (deterministic).
+ * max_seqlen_k (flash_attn_varlen_func's argument; 0 = unknown) only steers that schedule.
+ */
+int flite_attn_varlen_fwd_ws(void* stream, const void* q, const void* k, const void* v, void* o, long q_row_stride,
+                             long k_row_stride, long v_row_stride, long o_row_stride, long head_stride,
+                             const int* cu_seqlens_q, const int* cu_seqlens_k, int batch, int num_heads,
+                             int head_dim, int max_seqlen_q, int max_seqlen_k, float softmax_scale, float max_score,
+                             void* workspace, long workspace_bytes);
+
+/*
  * RMSNorm (+weight) (+adaLN modulate) to bf16: y = x*rsqrt(mean(x^2)+eps) * w * (1+scale) + shift.
  * Replaces LigerRMSNorm (model.py:238,248,260,437), RMSNorm (model.py:92-108) and the modulate
  * `norm_x * (1 + scale) + shift` (model.py:284,293,300,580). x is fp32 (x_is_bf16 = 0) or bf16.

@@ -154,6 +154,38 @@ def test_attention_varlen(lens_q, lens_k, bounded):
     assert rel(out, ref) < 1e-2
 
 
+# Tail split (attention.hip "Schedule"): the partial last q-tile of every (sequence, head) is cut by key ranges
+# over the chip and reduced in slab order. Cases: the DiT self (T = 4112: 16-row tails) and cross shapes, ragged
+# tails of up to 127 rows, more chunks than key tiles (empty chunks), no keys at all.
+@pytest.mark.parametrize("lens_q,lens_k,H", [([4112, 4112], None, 12), ([4112, 4112], [512, 512], 12),
+                                             ([300, 200], None, 2), ([130, 255], [24, 17], 2),
+                                             ([1000, 77], [700, 0], 3), ([50], [4096], 1)])
+def test_attention_tail_split(lens_q, lens_k, H):
+    D = 256
+    self_attn = lens_k is None
+    lens_k = lens_q if self_attn else lens_k
+    B = len(lens_q)
+    ws = nat.attn_workspace(DEV, B, H)
+    assert ws is not None  # every case here is small enough in B*H for the split
+    cu_q = torch.tensor([0] + list(torch.tensor(lens_q).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lens_k).cumsum(0)), dtype=torch.int32)
+    g = torch.Generator(device=DEV).manual_seed(sum(lens_q) + H)
+    q = R.own_rmsnorm(torch.randn(int(cu_q[-1]), H, D, device=DEV, generator=g), None).bfloat16()
+    k = R.own_rmsnorm(torch.randn(max(int(cu_k[-1]), 1), H, D, device=DEV, generator=g), None).bfloat16()
+    v = torch.randn(max(int(cu_k[-1]), 1), H, D, device=DEV, generator=g).bfloat16()
+    args = (q, k, v, cu_q.to(DEV), cu_k.to(DEV), max(lens_q), D ** -0.5)
+    split = nat.attn_varlen(*args, max_score=16.5, workspace=ws)
+    whole = nat.attn_varlen(*args, max_score=16.5)
+    if sum(lens_q) * H * max(lens_k) <= 2 * 4112 * 4112 * 2:
+        ref = _attn_ref(q, k, v, cu_q, cu_k, D ** -0.5)
+        assert rel(split, ref) < 1e-2
+    assert rel(split, whole) < 5e-3  # same math, only the summation order of the tail rows differs
+    # deterministic (fixed slab order) and the workspace is left zeroed for the next launch
+    again = nat.attn_varlen(*args, max_score=16.5, workspace=ws)
+    assert torch.equal(split, again)
+    assert int(ws[:4096].view(torch.int32).abs().sum().item()) == 0
+
+
 def test_attention_spike_rescale():
     # force the online-softmax rescale: one key far above the rest in a late tile (§5.4 rule 26)
     H, D, L = 1, 256, 700
