@@ -121,7 +121,7 @@ struct GemmCta {
   __device__ __forceinline__ GemmCta(const GemmParams& p_, char* smem) : p(p_) {
     tid = threadIdx.x;
     lane = tid & 63;
-    wave = tid >> 6;
+    wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     wave_m = wave >> 2;  // 0..1
     wave_n = wave & 3;   // 0..3
     lr = lane & 15;
@@ -268,7 +268,9 @@ struct GemmCta {
     interleave<4>();
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    stage(kt + 2, BUF);
+    // The two waves of a SIMD (w, w + 4) issue their copies of tile t+2 a half-step apart, so one of them
+    // keeps the MFMA pipe fed while the other spends issue cycles on LDS-DMA.
+    stage(wave_m == 0 ? kt + 2 : ke, BUF);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       wx[i] = rd_w<BUF ^ 1>(0, i);
@@ -276,6 +278,7 @@ struct GemmCta {
     }
     mfma_half(acc, wy, ah, 4);
     interleave<8>();
+    stage(wave_m == 1 ? kt + 2 : ke, BUF);
   }
 
   // acc = A[m0.., kb*64 : kend*64] . W[n0.., same]^T  (setup_tile(m0, n0) first). Every k-tile runs the same
