@@ -82,6 +82,37 @@ __device__ __forceinline__ void blds16(const i32x4& rsrc, unsigned voff, unsigne
       : "memory");
 }
 
+// O^T += V^T . P^T with the accumulator pinned to AGPRs. Left to itself hipcc keeps O (128 registers per lane)
+// in VGPRs inside the key loop and copies it to and from AGPRs every tile (~300 v_accvgpr moves per tile,
+// an issue-bound loop). An MFMA reads its srcC from AGPRs directly. The asm is opaque to the hazard
+// recognizer, so: the first MFMA after the VALU that produced its P operand carries `s_nop 1` (VALU write ->
+// MFMA read), and every reader of O after the loop waits behind o_acc_fence() (MFMA write -> read).
+// The NOP form also "redefines" pk, so every other MFMA reading pk is ordered after it.
+template <bool NOP>
+__device__ __forceinline__ void mfma_o(f32x16& acc, const bf16x8& v, bf16x8& pk) {
+  if constexpr (NOP)
+    asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %2, %1, %0" : "+a"(acc), "+v"(pk) : "v"(v));
+  else
+    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(v), "v"(pk));
+}
+// S^T = K . Q^T with Q^T pinned to AGPRs (loop-invariant; hipcc otherwise shuttles it between the register files
+// every tile) and S in VGPRs for the softmax VALU.
+__device__ __forceinline__ void mfma_s_first(f32x16& acc, const bf16x8& k, const bf16x8& q) {
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(k), "a"(q));
+}
+__device__ __forceinline__ void mfma_s(f32x16& acc, const bf16x8& k, const bf16x8& q) {
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(k), "a"(q));
+}
+// Wait states between an asm MFMA's write and a VALU / v_accvgpr read of its result (XDL 32x32: 18). The
+// fence "redefines" the results, so no reader can be scheduled above it.
+__device__ __forceinline__ void mfma_read_fence(f32x16& a, f32x16& b) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void o_acc_fence(f32x16 (&o)[8]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+               : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]), "+a"(o[4]), "+a"(o[5]), "+a"(o[6]), "+a"(o[7]));
+}
+
 __device__ __forceinline__ unsigned lds_addr_of(const void* p) {
   return (unsigned)(unsigned long long)(const LDS_AS char*)p;
 }
@@ -175,6 +206,11 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     const bf16_t* qp = p.q + (long)(q_start + qc) * p.q_row_stride + (long)h * p.q_head_stride + 8 * hh;
 #pragma unroll
     for (int s = 0; s < 16; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+    if constexpr (BOUNDED) {  // move Q^T into AGPRs here, then clear the write -> MFMA-read hazard
+#pragma unroll
+      for (int s = 0; s < 16; ++s) asm volatile("" : "+a"(qf[s]));
+      asm volatile("s_nop 4" ::: "memory");
+    }
   }
 
   // ---- staging: 8 K + 8 V LDS-DMA pieces per wave per tile; piece qi covers tile rows 2qi, 2qi+1.
@@ -231,35 +267,89 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) v_off[dt] = (dt ^ vq) * 64;
 
-  auto compute = [&](const int buf) {
+  // BOUNDED: compute(buf, tn) also streams tile tn (tn < 0: none) into buffer buf ^ 1: the 8 K pieces in one
+  // burst at the start, the 8 V pieces one per MFMA pair over the first half of the S phase (an LDS-DMA costs
+  // ~60 issue cycles; an issue ~1 µs from the end-of-tile wait exposes its landing latency).
+  auto compute = [&](const int buf, const int tn) {
     const char* Kb = kbase + buf * TILE;
     const char* Vb = vbase + buf * TILE;
-    // S^T for both 32-key halves: all 32 K fragments first, two independent accumulation chains
+    i32x4 krs_n = {0, 0, 0, 0}, vrs_n = {0, 0, 0, 0};
+    if (BOUNDED && tn >= 0) {
+      const long rows_left = k_len - (long)tn * KT;
+      krs_n = make_rsrc(p.k + k_base + (long)tn * KT * p.k_row_stride,
+                        (unsigned)min(rows_left * p.k_row_stride * 2, 0x7fffffffL));
+      vrs_n = make_rsrc(p.v + v_base + (long)tn * KT * p.v_row_stride,
+                        (unsigned)min(rows_left * p.v_row_stride * 2, 0x7fffffffL));
+    }
+    auto piece = [&](int i) {  // i < 8: K piece i, else V piece i - 8
+      if (tn >= 0) {
+        const unsigned dst = lds0 + (buf ^ 1) * TILE + (wave * 8 + (i & 7)) * 1024;
+        if (i < 8)
+          blds16(krs_n, k_src[i], dst + K_OFF);
+        else
+          blds16(vrs_n, v_src[i - 8], dst + V_OFF);
+      }
+    };
     f32x16 s0, s1;
+    if constexpr (BOUNDED) {
+      // S^T for both 32-key halves, two accumulation chains; K fragments 3 k-steps ahead of their MFMAs,
+      // order pinned by sched_barrier (the loop then holds ~24 K-fragment registers, not 128).
+      bf16x8 k0[16], k1[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = 0.f;
-      s1[r] = 0.f;
-    }
-    bf16x8 k0[16], k1[16];
+      for (int s = 0; s < 3; ++s) {
+        k0[s] = *(const bf16x8*)(Kb + k_off[s]);
+        k1[s] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      k0[s] = *(const bf16x8*)(Kb + k_off[s]);
-      k1[s] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s]);
-    }
+      for (int i = 0; i < 8; ++i) piece(i);  // K of the next tile: needed first, issued first
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0[s], qf[s], s0, 0, 0, 0);
-      s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1[s], qf[s], s1, 0, 0, 0);
-    }
-    // schedule: 8 fragment reads ahead, then MFMA pairs each followed by the next two reads
-    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+      for (int s = 0; s < 16; ++s) {
+        if (s + 3 < 16) {
+          k0[s + 3] = *(const bf16x8*)(Kb + k_off[s + 3]);
+          k1[s + 3] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s + 3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (s == 0) {
+          mfma_s_first(s0, k0[0], qf[0]);
+          mfma_s_first(s1, k1[0], qf[0]);
+        } else {
+          mfma_s(s0, k0[s], qf[s]);
+          mfma_s(s1, k1[s], qf[s]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (s < 8) piece(8 + s);  // V pieces in the first half of the S phase
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mfma_read_fence(s0, s1);  // MFMA write of S -> VALU read (exp below)
+    } else {
+      // S^T for both 32-key halves: all 32 K fragments first, two independent accumulation chains
 #pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = 0.f;
+        s1[r] = 0.f;
+      }
+      bf16x8 k0[16], k1[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        k0[s] = *(const bf16x8*)(Kb + k_off[s]);
+        k1[s] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s]);
+      }
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0[s], qf[s], s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1[s], qf[s], s1, 0, 0, 0);
+      }
+      // schedule: 8 fragment reads ahead, then MFMA pairs each followed by the next two reads
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
     if constexpr (!BOUNDED) {
       float tmax = -INFINITY;
 #pragma unroll
@@ -300,7 +390,14 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         for (int dt = 0; dt < 8; ++dt) {
           const s16x8 c = __builtin_shufflevector(lo[dt], hi[dt], 0, 1, 2, 3, 4, 5, 6, 7);
           const bf16x8 vf = __builtin_bit_cast(bf16x8, c);
-          o_acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pk, o_acc[dt], 0, 0, 0);
+          if constexpr (BOUNDED) {  // O stays in AGPRs (no VALU ever touches it inside the loop)
+            if (dt == 0)
+              mfma_o<true>(o_acc[dt], vf, pk);
+            else
+              mfma_o<false>(o_acc[dt], vf, pk);
+          } else {  // the online rescale multiplies O by VALU every tile
+            o_acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pk, o_acc[dt], 0, 0, 0);
+          }
         }
         // 16 transposed reads: 4 ahead, then one MFMA per two reads
         __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
@@ -318,20 +415,36 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     stage(t_begin, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int j = 0; j < nt; j += 2) {
-      if (j + 1 < nt) stage(t_begin + j + 1, 1);
-      compute(0);
+    // two tiles per iteration (static LDS buffer index), one exit; an odd last tile is peeled
+    int j = 0;
+    for (; j + 1 < nt; j += 2) {
+      if constexpr (BOUNDED) {
+        compute(0, t_begin + j + 1);
+      } else {
+        stage(t_begin + j + 1, 1);
+        compute(0, -1);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (j + 1 >= nt) break;
-      if (j + 2 < nt) stage(t_begin + j + 2, 0);
-      compute(1);
+      const int t2 = j + 2 < nt ? t_begin + j + 2 : -1;
+      if constexpr (BOUNDED) {
+        compute(1, t2);
+      } else {
+        if (t2 >= 0) stage(t2, 0);
+        compute(1, -1);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (j < nt) {
+      compute(0, -1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   }
 
   ATTN_STAMP(1);
+  if constexpr (BOUNDED) o_acc_fence(o_acc);
   // keys past the end were staged as zero rows: each contributed exp2(0*sl2 - m) to l and 0 to O
   l_run += __shfl_xor(l_run, 32, 64);  // the two lane halves hold the sums of complementary keys
   const int n_pad = nt > 0 ? max(0, t_end * KT - k_len) : 0;

@@ -38,6 +38,10 @@ def run(T, Lk, H=12, iters=20, bounded=True, split=False):
 
 
 if __name__ == "__main__":
+    if "--only" in sys.argv:  # one configuration (counter passes): --only T Lk
+        i = sys.argv.index("--only")
+        run(int(sys.argv[i + 1]), int(sys.argv[i + 2]), iters=5, split=True)
+        sys.exit(0)
     for b, sp in ((False, False), (True, False), (True, True)):
         run(4112, 4112, bounded=b, split=sp)
         run(4112, 512, bounded=b, split=sp)
