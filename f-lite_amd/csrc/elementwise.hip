@@ -80,45 +80,135 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(NormModParams p) {
   }
 }
 
+// Same operation, one 256-thread workgroup per output row, for D = 1024 * NQ (the DiT width 3072: NQ = 3).
+// Thread t holds elements q*1024 + 4t .. +3 (q < NQ): 12 fp32 registers of x instead of 48, so 8 waves per
+// SIMD stay resident and every wave has all of its row loads in flight at once; the row sum of squares is
+// a wave reduction plus 4 partials through LDS.
+template <bool IN_BF16, int NQ>
+__global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
+  __shared__ float part[4];
+  const int t = threadIdx.x;
+  const long m = blockIdx.x;
+  const long seg = p.in_seg > 0 ? m / p.in_seg : 0;
+  const long in_row = p.in_seg > 0 ? seg * p.in_stride + p.in_off + (m % p.in_seg) : m;
+  float v[4 * NQ];
+  if constexpr (IN_BF16) {
+    const bf16_t* xr = (const bf16_t*)p.x + in_row * p.ldx;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const u32x2 w = *(const u32x2*)(xr + q * 1024 + t * 4);
+      v[4 * q + 0] = __uint_as_float(w.x << 16);
+      v[4 * q + 1] = __uint_as_float(w.x & 0xffff0000u);
+      v[4 * q + 2] = __uint_as_float(w.y << 16);
+      v[4 * q + 3] = __uint_as_float(w.y & 0xffff0000u);
+    }
+  } else {
+    const float* xr = (const float*)p.x + in_row * p.ldx;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const f32x4 w = *(const f32x4*)(xr + q * 1024 + t * 4);
+      v[4 * q + 0] = w[0];
+      v[4 * q + 1] = w[1];
+      v[4 * q + 2] = w[2];
+      v[4 * q + 3] = w[3];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4 * NQ; ++i) ss += v[i] * v[i];
+  ss = wave_sum(ss);
+  if ((t & 63) == 0) part[t >> 6] = ss;
+  __syncthreads();
+  ss = part[0] + part[1] + part[2] + part[3];
+  const float r = rsqrtf(ss / (float)(1024 * NQ) + p.eps);
+  const float* shift = p.shift ? p.shift + seg * p.mod_seg_stride : nullptr;
+  const float* scale = p.scale ? p.scale + seg * p.mod_seg_stride : nullptr;
+  bf16_t* yr = p.y + m * p.ldy;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int n = q * 1024 + t * 4;
+    float wgt[4] = {1.f, 1.f, 1.f, 1.f};
+    if (p.w) {
+      const u32x2 ww = *(const u32x2*)(p.w + n);
+      wgt[0] = __uint_as_float(ww.x << 16);
+      wgt[1] = __uint_as_float(ww.x & 0xffff0000u);
+      wgt[2] = __uint_as_float(ww.y << 16);
+      wgt[3] = __uint_as_float(ww.y & 0xffff0000u);
+    }
+    f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sh = {0.f, 0.f, 0.f, 0.f};
+    if (scale) sc = *(const f32x4*)(scale + n);
+    if (shift) sh = *(const f32x4*)(shift + n);
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = v[4 * q + j] * r * wgt[j] * (1.f + sc[j]) + sh[j];
+    u32x2 st;
+    st.x = pack2bf(o[0], o[1]);
+    st.y = pack2bf(o[2], o[3]);
+    *(u32x2*)(yr + n) = st;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // RoPE (2-D, rotate-half pairs (j, j+128), rotation by -theta) + per-head RMSNorm (no weight), in place
 // on bf16 heads of 256. Reference: apply_rotary_emb (model.py:403-414) then QKNorm (model.py:115-126,180,197).
-// One wave per (row, head); lane l holds elements 4(l&31)+i of half (l>>5) -> the rotation partner is
-// lane l^32.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rope_qknorm_kernel(RopeNormParams p) {
+// 16 B per lane: a half-wave per head, two heads per wave. Lane s = lane & 31 of its half
+// holds elements 8(s&15) .. +7 of head half (s>>4), so its rotation partner is lane ^ 16 and the head's sum of
+// squares is a 32-lane reduction.
+__global__ __launch_bounds__(256) void rope_qknorm16_kernel(RopeNormParams p) {
   const int lane = threadIdx.x & 63;
-  const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const long total = (long)p.rows * p.heads;
+  const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // (row, head pair)
+  const int pairs = (p.heads + 1) >> 1;
+  const long total = (long)p.rows * pairs;
   if (item >= total) return;
-  const long row = item / p.heads;
-  const int head = (int)(item % p.heads);
-  bf16_t* xp = p.x + row * p.ldx + (long)head * 256 + lane * 4;
-  const u32x2 w = *(const u32x2*)xp;
-  float v[4] = {__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
-                __uint_as_float(w.y & 0xffff0000u)};
+  const long row = item / pairs;
+  const int head = (int)(item % pairs) * 2 + (lane >> 5);
+  const int s = lane & 31;
+  const int part = s >> 4;
+  const int j0 = 8 * (s & 15);  // angle index of this lane's first element
+  const bool live = head < p.heads;
+  bf16_t* xp = p.x + row * p.ldx + (long)min(head, p.heads - 1) * 256 + 128 * part + j0;
+  const u32x4 w = *(const u32x4*)xp;
+  float v[8];
+  v[0] = __uint_as_float(w.x << 16);
+  v[1] = __uint_as_float(w.x & 0xffff0000u);
+  v[2] = __uint_as_float(w.y << 16);
+  v[3] = __uint_as_float(w.y & 0xffff0000u);
+  v[4] = __uint_as_float(w.z << 16);
+  v[5] = __uint_as_float(w.z & 0xffff0000u);
+  v[6] = __uint_as_float(w.w << 16);
+  v[7] = __uint_as_float(w.w & 0xffff0000u);
   if (p.cos != nullptr && head < p.rope_heads) {
     const long tok = row % p.tokens_per_seq;
-    const int j = 4 * (lane & 31);
-    const f32x4 c = *(const f32x4*)(p.cos + tok * 128 + j);
-    const f32x4 s = *(const f32x4*)(p.sin + tok * 128 + j);
-    float o[4];
+    const f32x4 c0 = *(const f32x4*)(p.cos + tok * 128 + j0);
+    const f32x4 c1 = *(const f32x4*)(p.cos + tok * 128 + j0 + 4);
+    const f32x4 s0 = *(const f32x4*)(p.sin + tok * 128 + j0);
+    const f32x4 s1 = *(const f32x4*)(p.sin + tok * 128 + j0 + 4);
+    const float c[8] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+    const float sn[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    float o[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float partner = __shfl_xor(v[i], 32, 64);
-      // lanes < 32 hold x1 (y1 = x1 c + x2 s); lanes >= 32 hold x2 (y2 = -x1 s + x2 c)
-      o[i] = (lane < 32) ? (v[i] * c[i] + partner * s[i]) : (-partner * s[i] + v[i] * c[i]);
+    for (int i = 0; i < 8; ++i) {
+      const float partner = __shfl_xor(v[i], 16, 64);
+      // first half holds x1 (y1 = x1 c + x2 s); second half holds x2 (y2 = -x1 s + x2 c)
+      o[i] = part == 0 ? (v[i] * c[i] + partner * sn[i]) : (-partner * sn[i] + v[i] * c[i]);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = o[i];
+    for (int i = 0; i < 8; ++i) v[i] = o[i];
   }
-  float ss = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
-  ss = wave_sum(ss);
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss += v[i] * v[i];
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
   const float r = rsqrtf(ss * (1.f / 256.f) + p.eps);
-  u32x2 st;
+  if (!live) return;
+  u32x4 st;
   st.x = pack2bf(v[0] * r, v[1] * r);
   st.y = pack2bf(v[2] * r, v[3] * r);
-  *(u32x2*)xp = st;
+  st.z = pack2bf(v[4] * r, v[5] * r);
+  st.w = pack2bf(v[6] * r, v[7] * r);
+  *(u32x4*)xp = st;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -363,8 +453,16 @@ int grid_for(long total, int per_block = 256) {
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   FLITE_REQUIRE(p.ldx % 4 == 0 && p.ldy % 4 == 0, "rmsnorm: strides must be multiples of 4");
   if (p.rows <= 0) return 0;
+  if (p.D == 3072 && p.rows < (1L << 31)) {  // the DiT width: one workgroup per row
+    if (in_bf16)
+      hipLaunchKernelGGL((rmsnorm_mod_row_kernel<true, 3>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
+    FLITE_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
   const int grid = (int)((p.rows + 3) / 4);
-#define FLITE_NORM_CASE(N)                                                                       \
+#define FLITE_NORM_CASE(N)                                                                      \
   case N:                                                                                        \
     if (in_bf16)                                                                                 \
       hipLaunchKernelGGL((rmsnorm_mod_kernel<true, N>), dim3(grid), dim3(256), 0, s, p);         \
@@ -392,9 +490,10 @@ int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
 int rope_qknorm(const RopeNormParams& p, hipStream_t s) {
   FLITE_REQUIRE(p.ldx % 4 == 0, "rope_qknorm: stride must be a multiple of 4");
   if (p.cos) FLITE_REQUIRE(p.tokens_per_seq > 0, "rope_qknorm: tokens_per_seq must be > 0");
-  const long items = (long)p.rows * p.heads;
+  const long items = (long)p.rows * ((p.heads + 1) / 2);
   if (items <= 0) return 0;
-  hipLaunchKernelGGL(rope_qknorm_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, p);
+  FLITE_REQUIRE(p.ldx % 8 == 0 && ((uintptr_t)p.x & 15) == 0, "rope_qknorm: rows must be 16-B aligned");
+  hipLaunchKernelGGL(rope_qknorm16_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, p);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

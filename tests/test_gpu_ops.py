@@ -201,9 +201,10 @@ def test_attention_spike_rescale():
     assert rel(out, ref) < 1e-2
 
 
+@pytest.mark.parametrize("D", [512, 3072])  # 3072: the one-workgroup-per-row kernel of the DiT width
 @pytest.mark.parametrize("in_bf16", [False, True])
-def test_rmsnorm_modulate(in_bf16):
-    rows, D, T = 600, 512, 250
+def test_rmsnorm_modulate(in_bf16, D):
+    rows, T = 600, 250
     x = torch.randn(rows, D, device=DEV) * 3
     if in_bf16:
         x = x.bfloat16()
@@ -229,8 +230,9 @@ def test_rope_tables_match_reference(golden):
     assert mism < 1e-3  # bf16 rounding of 1-ulp-different fp32 values can flip a handful of entries
 
 
-def test_rope_qknorm():
-    rows, H, T = 300, 2, 150
+@pytest.mark.parametrize("H", [2, 3, 12])  # heads run in pairs: odd counts leave a half-empty pair
+def test_rope_qknorm(H):
+    rows, T = 300, 150
     x = torch.randn(rows, 3 * H * 256, device=DEV).bfloat16()
     cos, sin = nat.rope_tables(12, 13, 16, 10000.0, round_bf16=True)
     assert cos.shape[0] >= T
@@ -245,6 +247,18 @@ def test_rope_qknorm():
         got = y.float().cpu().reshape(rows, 3, H, 256)[:, part]
         assert rel(got, ref) < 4e-3
     assert torch.equal(y[:, 2 * H * 256:], x[:, 2 * H * 256:])  # v untouched
+    # norm only (cross-attention q), odd head count, rotation on a prefix of the heads
+    z = x.clone()
+    nat.rope_qknorm_(z, heads=H, rope_heads=0)
+    refq = R.own_rmsnorm(xc[:, 0], None)
+    assert rel(z.float().cpu().reshape(rows, 3, H, 256)[:, 0], refq) < 4e-3
+    assert torch.equal(z[:, H * 256:], x[:, H * 256:])
+    if H >= 2:
+        u = x.clone()
+        nat.rope_qknorm_(u, heads=H, rope_heads=1, cos=cos, sin=sin, tokens_per_seq=T)
+        got = u.float().cpu().reshape(rows, 3, H, 256)[:, 0]
+        assert rel(got[:, :1], R.own_rmsnorm(R.apply_rotary_emb(xc[:, 0, :1], c, s), None)) < 4e-3
+        assert rel(got[:, 1:], R.own_rmsnorm(xc[:, 0, 1:], None)) < 4e-3
 
 
 def test_timestep_embedding_quantized(golden):
