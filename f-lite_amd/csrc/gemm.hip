@@ -313,6 +313,59 @@ struct GemmCta {
     if (kt < kend) ktile<0>(acc, wx, wy, al, ah, kt);
   }
 
+  // Gated residual x[m][n] += gate[seg(m)][n] * (acc + bias[n]) (model.py:289,297,301). A read-modify-write of
+  // the fp32 residual: the loads of two accumulator rows (8 x + 8 gate, 16 B per lane) are issued together at
+  // clamped, always-valid addresses and only the stores are masked, so the tile pays 4 memory round trips
+  // instead of one per 16-B group (a bounds branch around each load makes hipcc wait vmcnt(0) per group).
+  template <bool GATED>
+  __device__ __forceinline__ void resid_epilogue(const f32x4 (&acc)[8][4], int m_base, int n_base) {
+    float bias[4][4];
+    int nc[4];
+    bool nok[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n_base + ni * 16;
+      nok[ni] = n < p.N;  // N % 4 == 0: a 4-column group is entirely in or out
+      nc[ni] = nok[ni] ? n : 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[ni][r] = (p.bias != nullptr && nok[ni]) ? bf2f(p.bias[nc[ni] + r]) : 0.f;
+    }
+#pragma unroll
+    for (int mb = 0; mb < 8; mb += 2) {
+      f32x4 xv[2][4], gv[2][4];
+      float* orow[2];
+      bool mok[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int m = m_base + (mb + i) * 16;
+        mok[i] = m < p.M;
+        const int mc = mok[i] ? m : p.M - 1;
+        orow[i] = (float*)p.out + (long)mc * p.ldo;
+        const float* grow = GATED ? p.gate + (long)(mc / p.rows_per_seg) * p.gate_seg_stride : nullptr;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          xv[i][ni] = *(const f32x4*)(orow[i] + nc[ni]);
+          if constexpr (GATED) gv[i][ni] = *(const f32x4*)(grow + nc[ni]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          f32x4 x = xv[i][ni];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = acc[mb + i][ni][r] + bias[ni][r];
+            if constexpr (GATED)
+              x[r] += v * gv[i][ni][r];
+            else
+              x[r] += v;
+          }
+          if (mok[i] && nok[ni]) *(f32x4*)(orow[i] + nc[ni]) = x;
+        }
+    }
+  }
+
   // ---- epilogue: lane holds C[m][n..n+3] for m = m_base + mi*16 + (lane&15), n = n_base + ni*16 + 4*(lane>>4)
   __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], int m0, int n0) {
     const int m_base = m0 + wave_m * 128 + lr;
@@ -339,6 +392,12 @@ struct GemmCta {
         }
       }
       return;
+    } else if constexpr (EPI == EPI_RESID_F32) {
+      if (p.gate != nullptr)
+        resid_epilogue<true>(acc, m_base, n_base);
+      else
+        resid_epilogue<false>(acc, m_base, n_base);
+      return;
     } else {
       float bias[4][4];
 #pragma unroll
@@ -353,10 +412,6 @@ struct GemmCta {
         const int m = m_base + mi * 16;
         if (m >= p.M) continue;
         const long om = p.out_seg > 0 ? (m / p.out_seg) * p.out_seg_stride + p.out_seg_off + (m % p.out_seg) : m;
-        const float* grow = nullptr;
-        if constexpr (EPI == EPI_RESID_F32) {
-          if (p.gate != nullptr) grow = p.gate + (long)(m / p.rows_per_seg) * p.gate_seg_stride;
-        }
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           const int n = n_base + ni * 16;
@@ -391,18 +446,6 @@ struct GemmCta {
             } else {
               for (int r = 0; r < 4 && n + r < p.N; ++r) o[r] = v[r];
             }
-          } else if constexpr (EPI == EPI_RESID_F32) {
-            float* o = (float*)p.out + om * p.ldo + n;
-            f32x4 x = *(f32x4*)o;
-            if (grow != nullptr) {
-              const f32x4 g = *(const f32x4*)(grow + n);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) x[r] += v[r] * g[r];
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) x[r] += v[r];
-            }
-            *(f32x4*)o = x;
           }
         }
       }
@@ -681,6 +724,7 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
     case EPI_RESID_F32:
       FLITE_REQUIRE(p.N % 4 == 0 && p.ldo % 4 == 0, "gemm(resid): N, ldo must be multiples of 4");
       FLITE_REQUIRE(p.gate == nullptr || p.rows_per_seg > 0, "gemm(resid): rows_per_seg must be > 0");
+      FLITE_REQUIRE(p.out_seg == 0 && p.act == 0, "gemm(resid): no row remap or activation");
       launch<EPI_RESID_F32>(p, stream);
       break;
     case EPI_SWIGLU_BF16:

@@ -59,18 +59,21 @@ def bench(M, N, K, iters=20, epi=nat.EPI_STORE_BF16, rounds=5):
     a = torch.randn(M, K, device=dev).bfloat16()
     w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
     w2 = (torch.randn(N, K, device=dev) * 0.05).bfloat16() if epi == nat.EPI_SWIGLU_BF16 else None
-    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    resid = epi == nat.EPI_RESID_F32
+    out = torch.zeros(M, N, device=dev, dtype=torch.float32 if resid else torch.bfloat16)
+    gate = torch.randn(2, N, device=dev) if resid else None
+    kw = dict(gate=gate, gate_seg_stride=N, rows_per_seg=(M + 1) // 2) if resid else {}
     s = torch.cuda.Event(enable_timing=True); e = torch.cuda.Event(enable_timing=True)
     res = {"dp": [], "sk": []}
     for _ in range(rounds):
         for mode in ("dp", "sk"):
             ws = WS if mode == "sk" else None
             for _ in range(2):
-                nat.gemm(a, w, out=out, epilogue=epi, w2=w2, workspace=ws)
+                nat.gemm(a, w, out=out, epilogue=epi, w2=w2, workspace=ws, **kw)
             torch.cuda.synchronize()
             s.record()
             for _ in range(iters):
-                nat.gemm(a, w, out=out, epilogue=epi, w2=w2, workspace=ws)
+                nat.gemm(a, w, out=out, epilogue=epi, w2=w2, workspace=ws, **kw)
             e.record(); torch.cuda.synchronize()
             res[mode].append(s.elapsed_time(e) / iters)
     Nf = 2 * N if epi == nat.EPI_SWIGLU_BF16 else N
@@ -97,5 +100,7 @@ if __name__ == "__main__":
     bench(8224, 3072, 3072)
     bench(8224, 12288, 3072, epi=nat.EPI_SWIGLU_BF16)
     bench(8224, 3072, 12288)
+    bench(8224, 3072, 3072, epi=nat.EPI_RESID_F32)
+    bench(8224, 3072, 12288, epi=nat.EPI_RESID_F32)
     bench(8192, 8192, 8192, iters=10)
     bench(8224, 1536, 3072, epi=nat.EPI_SWIGLU_BF16)
