@@ -16,6 +16,7 @@
 // the per-lane SOURCE offset and undone on the ds_read), two LDS buffers, one barrier per 64-deep k-tile.
 // Fragments are register double-buffered at half-k-step granularity (W: two sets of 4; A: low/high halves of
 // 8), so every ds_read overlaps MFMAs of the previous half-step, including across the k-tile barrier.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -630,6 +631,9 @@ int choose_sk_tiles(const GemmParams& p, int T) {
   if (rem == 0) return 0;
   const double nk = p.K / BK;
   if (rem * nk < 2.0 * G) return 0;  // ranges of at least 2 k-tiles
+#ifdef FLITE_SK_STAMPS
+  if (getenv("FLITE_SK_FORCE") != nullptr) return rem;  // diagnostic build: time the split where it is not taken
+#endif
   const double dp = (double)(T / G + 1) * nk;
   const double sk = (double)(T / G) * nk + 1.1 * rem * nk / G + 24.0;
   return sk < 0.97 * dp ? rem : 0;
