@@ -270,8 +270,12 @@ struct GemmCta {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // The two waves of a SIMD (w, w + 4) issue their copies of tile t+2 a half-step apart, so one of them
-    // keeps the MFMA pipe fed while the other spends issue cycles on LDS-DMA.
-    stage(wave_m == 0 ? kt + 2 : ke, BUF);
+    // keeps the MFMA pipe fed while the other spends issue cycles on LDS-DMA. Not in CONV mode: there the
+    // per-tap gather addressing makes the split schedule 1.9x slower (tools/kbench_conv.py).
+    if constexpr (CONV)
+      stage(kt + 2, BUF);
+    else
+      stage(wave_m == 0 ? kt + 2 : ke, BUF);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       wx[i] = rd_w<BUF ^ 1>(0, i);
@@ -279,7 +283,7 @@ struct GemmCta {
     }
     mfma_half(acc, wy, ah, 4);
     interleave<8>();
-    stage(wave_m == 1 ? kt + 2 : ke, BUF);
+    if constexpr (!CONV) stage(wave_m == 1 ? kt + 2 : ke, BUF);
   }
 
   // acc = A[m0.., kb*64 : kend*64] . W[n0.., same]^T  (setup_tile(m0, n0) first). Every k-tile runs the same
