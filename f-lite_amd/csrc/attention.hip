@@ -282,7 +282,11 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
                         (unsigned)min(rows_left * p.v_row_stride * 2, 0x7fffffffL));
     }
     auto piece = [&](int i) {  // i < 8: K piece i, else V piece i - 8
+#ifdef FLITE_ATTN_ABL_NODMA
+      if (false) {
+#else
       if (tn >= 0) {
+#endif
         const unsigned dst = lds0 + (buf ^ 1) * TILE + (wave * 8 + (i & 7)) * 1024;
         if (i < 8)
           blds16(krs_n, k_src[i], dst + K_OFF);
@@ -370,10 +374,18 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       f32x16& sacc = kh ? s1 : s0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
+#ifdef FLITE_ATTN_ABL_NOEXP
+        const float e = sacc[r];
+#else
         const float e = __builtin_amdgcn_exp2f(sacc[r] * sl2 - m_run);
+#endif
         sacc[r] = e;
         l_run += e;
       }
+#ifdef FLITE_ATTN_ABL_NOPV
+      asm volatile("" : "+v"(sacc));
+      continue;
+#endif
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 pk;
@@ -411,6 +423,173 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     }
   };
 
+#ifdef FLITE_ATTN_ABL_NOBAR
+#define ATTN_TILE_SYNC() \
+  do {                   \
+  } while (0)
+#else
+#define ATTN_TILE_SYNC()                                \
+  do {                                                  \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    __syncthreads();                                    \
+  } while (0)
+#endif
+#ifndef FLITE_ATTN_OLDLOOP
+  if constexpr (BOUNDED) {
+    // ---- software-pipelined key loop (bounded softmax) ----
+    // Iteration j: phase A issues S_{j+1} = K_{j+1} . Q^T (K fragments from LDS) and, spread one per MFMA pair,
+    // the LDS-DMA copies of K_{j+2} and V_{j+1}; phase B runs O^T += V_j^T . P_j^T (V^T fragments by transposed
+    // LDS reads) and, one element per MFMA, the softmax of S_{j+1} (exp2, row sum, bf16 pack into P_{j+1}).
+    // Each phase then carries about the same issue load beside its 32 MFMAs. LDS ring: phase A reads
+    // Kbuf[(j+1)&1] while K_{j+2} lands in Kbuf[j&1]; phase B reads Vbuf[j&1] while V_{j+1} lands in
+    // Vbuf[(j+1)&1]; every buffer a copy overwrites was last read in iteration j-1, so one vmcnt(0) + barrier per
+    // iteration suffices. Every sum and its order are those of the unpipelined loop: the output is
+    // bit-identical to it.
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using BT = std::integral_constant<bool, true>;
+    using BF = std::integral_constant<bool, false>;
+    auto rsrc_tile = [&](const bf16_t* base, long off, long stride, int t, bool live) {
+      const long rows_left = live ? k_len - (long)t * KT : 0;
+      return make_rsrc(base + off + (long)t * KT * stride, (unsigned)max(0L, min(rows_left * stride * 2, 0x7fffffffL)));
+    };
+    f32x16 s0, s1;          // S of the tile whose softmax is pending
+    u32x4 pa[4], pb[4];     // P^T operands (kh, 16-key half) of two consecutive tiles, bf16 pairs
+    // phase A. KB: K buffer read by the S MFMAs; DKB / DVB: buffers the K / V copies land in; DMA: copies issued
+    auto phase_a = [&](auto kb_, auto dkb_, auto dvb_, auto dma_, int tk, bool k_live, int tv, bool v_live) {
+      constexpr int KB = decltype(kb_)::value, DKB = decltype(dkb_)::value, DVB = decltype(dvb_)::value;
+      constexpr bool DMA = decltype(dma_)::value;
+      const char* Kb = kbase + KB * TILE;
+      i32x4 krs = {0, 0, 0, 0}, vrs = {0, 0, 0, 0};
+      if constexpr (DMA) {
+        krs = rsrc_tile(p.k, k_base, p.k_row_stride, tk, k_live);
+        vrs = rsrc_tile(p.v, v_base, p.v_row_stride, tv, v_live);
+      }
+      bf16x8 k0[16], k1[16];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        k0[s] = *(const bf16x8*)(Kb + k_off[s]);
+        k1[s] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        if (s + 3 < 16) {
+          k0[s + 3] = *(const bf16x8*)(Kb + k_off[s + 3]);
+          k1[s + 3] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s + 3]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (s == 0) {
+          mfma_s_first(s0, k0[0], qf[0]);
+          mfma_s_first(s1, k1[0], qf[0]);
+        } else {
+          mfma_s(s0, k0[s], qf[s]);
+          mfma_s(s1, k1[s], qf[s]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (DMA) {  // K pieces first (needed first), then V
+          if (s < 8)
+            blds16(krs, k_src[s], lds0 + DKB * TILE + (wave * 8 + s) * 1024 + K_OFF);
+          else
+            blds16(vrs, v_src[s - 8], lds0 + DVB * TILE + (wave * 8 + s - 8) * 1024 + V_OFF);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mfma_read_fence(s0, s1);  // MFMA write of S -> VALU read (softmax in the next phase B)
+    };
+    // softmax of key e (0..31: half e >> 4, row r = e & 15) of the pending S into the P^T operand pn
+    auto softmax_elem = [&](u32x4 (&pn)[4], int e, float& e_prev) {
+      const f32x16& sacc = e < 16 ? s0 : s1;
+      const int r = e & 15;
+      const float v = __builtin_amdgcn_exp2f(sacc[r] * sl2 - m_run);
+      l_run += v;
+      if (e & 1) {
+        const bf16x2 pr = {(__bf16)e_prev, (__bf16)v};
+        pn[(e >> 4) * 2 + (r >> 3)][(r & 7) >> 1] = __builtin_bit_cast(unsigned, pr);
+      }
+      e_prev = v;
+    };
+    // phase B: O^T += V^T . P^T (operand pc) from Vbuf[VB]; EX: the softmax of the pending S into pn
+    auto phase_b = [&](auto vb_, auto ex_, u32x4 (&pc)[4], u32x4 (&pn)[4]) {
+      constexpr int VB = decltype(vb_)::value;
+      constexpr bool EX = decltype(ex_)::value;
+      const char* Vb = vbase + VB * TILE;
+      float e_prev = 0.f;
+      // MFMA m = 8 g + dt, g = (kh, s): V^T fragment from rows kh*32 + 16 s (+8), d-tile dt; reads 2 MFMAs ahead
+      s16x4 lo[32], hi[32];
+      auto rd = [&](int m) {
+        const int g = m >> 3, dt = m & 7, kh = g >> 1, s = g & 1;
+        lo[m] = ds_tr16(Vb + (kh * 32 + 16 * s) * 512 + v_off[dt]);
+        hi[m] = ds_tr16(Vb + (kh * 32 + 16 * s + 8) * 512 + v_off[dt]);
+      };
+      rd(0);
+      rd(1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 32; ++m) {
+        if (m + 2 < 32) rd(m + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        const int g = m >> 3, dt = m & 7;
+        const s16x8 c = __builtin_shufflevector(lo[m], hi[m], 0, 1, 2, 3, 4, 5, 6, 7);
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, c);
+        bf16x8 pk = __builtin_bit_cast(bf16x8, pc[g]);
+        if (dt == 0)
+          mfma_o<true>(o_acc[dt], vf, pk);
+        else
+          mfma_o<false>(o_acc[dt], vf, pk);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (EX) softmax_elem(pn, m, e_prev);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // iteration j (parity P): phase A for S_{j+1} (HS) and phase B for PV_j with the softmax of S_{j+1}
+    auto iter = [&](auto par_, auto hs_, int j) {
+      constexpr int P = decltype(par_)::value;
+      constexpr bool HS = decltype(hs_)::value;
+      if constexpr (HS) {
+        if constexpr (P == 0)
+          phase_a(I1{}, I0{}, I1{}, BT{}, t_begin + j + 2, j + 2 < nt, t_begin + j + 1, true);
+        else
+          phase_a(I0{}, I1{}, I0{}, BT{}, t_begin + j + 2, j + 2 < nt, t_begin + j + 1, true);
+      }
+      if constexpr (P == 0)
+        phase_b(I0{}, hs_, pa, pb);
+      else
+        phase_b(I1{}, hs_, pb, pa);
+      ATTN_TILE_SYNC();
+    };
+    if (nt > 0) {
+      // prologue: K_0, V_0 into buffer 0 and K_1 into Kbuf 1; S_0 and its softmax into pa
+      stage(t_begin, 0);
+      {
+        const i32x4 krs = rsrc_tile(p.k, k_base, p.k_row_stride, t_begin + 1, nt > 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) blds16(krs, k_src[i], lds0 + TILE + (wave * 8 + i) * 1024 + K_OFF);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      phase_a(I0{}, I0{}, I0{}, BF{}, 0, false, 0, false);
+      {
+        float e_prev = 0.f;
+#pragma unroll
+        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);
+      }
+      __syncthreads();  // every wave's K_0 reads are done before iteration 0 refills Kbuf 0
+      int j = 0;
+      for (; j + 2 < nt; j += 2) {
+        iter(I0{}, BT{}, j);
+        iter(I1{}, BT{}, j + 1);
+      }
+      if (nt - j == 2) {
+        iter(I0{}, BT{}, j);
+        iter(I1{}, BF{}, j + 1);
+      } else {
+        iter(I0{}, BF{}, j);
+      }
+    }
+  } else
+#endif
   if (nt > 0) {
     stage(t_begin, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -424,8 +603,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         stage(t_begin + j + 1, 1);
         compute(0, -1);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      ATTN_TILE_SYNC();
       const int t2 = j + 2 < nt ? t_begin + j + 2 : -1;
       if constexpr (BOUNDED) {
         compute(1, t2);
@@ -433,13 +611,11 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         if (t2 >= 0) stage(t2, 0);
         compute(1, -1);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      ATTN_TILE_SYNC();
     }
     if (j < nt) {
       compute(0, -1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      ATTN_TILE_SYNC();
     }
   }
 

@@ -42,6 +42,10 @@ if __name__ == "__main__":
         i = sys.argv.index("--only")
         run(int(sys.argv[i + 1]), int(sys.argv[i + 2]), iters=5, split=True)
         sys.exit(0)
+    if "--quick" in sys.argv:  # the bounded self-attention shape: whole rounds only, then with the split tail
+        run(4096, 4112, iters=50, split=False)
+        run(4112, 4112, iters=50, split=True)
+        sys.exit(0)
     for b, sp in ((False, False), (True, False), (True, True)):
         run(4112, 4112, bounded=b, split=sp)
         run(4112, 512, bounded=b, split=sp)
