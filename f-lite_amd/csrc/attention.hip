@@ -454,6 +454,15 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       const long rows_left = live ? k_len - (long)t * KT : 0;
       return make_rsrc(base + off + (long)t * KT * stride, (unsigned)max(0L, min(rows_left * stride * 2, 0x7fffffffL)));
     };
+#ifndef ATTN_KAHEAD
+#define ATTN_KAHEAD 3  // K fragment reads issued this many k-steps ahead of their MFMA pair
+#endif
+#ifndef ATTN_VAHEAD
+#define ATTN_VAHEAD 4  // V^T transposed reads issued this many MFMAs ahead
+#endif
+#ifndef ATTN_VDMA_B
+#define ATTN_VDMA_B 0  // 1: the V copies go in phase B (one per 4 MFMAs) instead of phase A
+#endif
     f32x16 s0, s1;          // S of the tile whose softmax is pending
     u32x4 pa[4], pb[4];     // P^T operands (kh, 16-key half) of two consecutive tiles, bf16 pairs
     // phase A. KB: K buffer read by the S MFMAs; DKB / DVB: buffers the K / V copies land in; DMA: copies issued
@@ -468,16 +477,16 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       }
       bf16x8 k0[16], k1[16];
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
+      for (int s = 0; s < ATTN_KAHEAD; ++s) {
         k0[s] = *(const bf16x8*)(Kb + k_off[s]);
         k1[s] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s]);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        if (s + 3 < 16) {
-          k0[s + 3] = *(const bf16x8*)(Kb + k_off[s + 3]);
-          k1[s + 3] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s + 3]);
+        if (s + ATTN_KAHEAD < 16) {
+          k0[s + ATTN_KAHEAD] = *(const bf16x8*)(Kb + k_off[s + ATTN_KAHEAD]);
+          k1[s + ATTN_KAHEAD] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s + ATTN_KAHEAD]);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (s == 0) {
@@ -491,7 +500,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         if constexpr (DMA) {  // K pieces first (needed first), then V
           if (s < 8)
             blds16(krs, k_src[s], lds0 + DKB * TILE + (wave * 8 + s) * 1024 + K_OFF);
-          else
+          else if (!ATTN_VDMA_B)
             blds16(vrs, v_src[s - 8], lds0 + DVB * TILE + (wave * 8 + s - 8) * 1024 + V_OFF);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -511,10 +520,11 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       e_prev = v;
     };
     // phase B: O^T += V^T . P^T (operand pc) from Vbuf[VB]; EX: the softmax of the pending S into pn
-    auto phase_b = [&](auto vb_, auto ex_, u32x4 (&pc)[4], u32x4 (&pn)[4]) {
+    auto phase_b = [&](auto vb_, auto ex_, u32x4 (&pc)[4], u32x4 (&pn)[4], int tv, bool v_live) {
       constexpr int VB = decltype(vb_)::value;
       constexpr bool EX = decltype(ex_)::value;
       const char* Vb = vbase + VB * TILE;
+      const i32x4 vrs = ATTN_VDMA_B ? rsrc_tile(p.v, v_base, p.v_row_stride, tv, v_live) : i32x4{0, 0, 0, 0};
       float e_prev = 0.f;
       // MFMA m = 8 g + dt, g = (kh, s): V^T fragment from rows kh*32 + 16 s (+8), d-tile dt; reads 2 MFMAs ahead
       s16x4 lo[32], hi[32];
@@ -523,12 +533,12 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         lo[m] = ds_tr16(Vb + (kh * 32 + 16 * s) * 512 + v_off[dt]);
         hi[m] = ds_tr16(Vb + (kh * 32 + 16 * s + 8) * 512 + v_off[dt]);
       };
-      rd(0);
-      rd(1);
+#pragma unroll
+      for (int m = 0; m < ATTN_VAHEAD; ++m) rd(m);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < 32; ++m) {
-        if (m + 2 < 32) rd(m + 2);
+        if (m + ATTN_VAHEAD < 32) rd(m + ATTN_VAHEAD);
         __builtin_amdgcn_sched_barrier(0);
         const int g = m >> 3, dt = m & 7;
         const s16x8 c = __builtin_shufflevector(lo[m], hi[m], 0, 1, 2, 3, 4, 5, 6, 7);
@@ -540,6 +550,9 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
           mfma_o<false>(o_acc[dt], vf, pk);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (EX) softmax_elem(pn, m, e_prev);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ATTN_VDMA_B && (m & 3) == 1)
+          blds16(vrs, v_src[m >> 2], lds0 + (VB ^ 1) * TILE + (wave * 8 + (m >> 2)) * 1024 + V_OFF);
         __builtin_amdgcn_sched_barrier(0);
       }
     };
@@ -554,9 +567,9 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
           phase_a(I0{}, I1{}, I0{}, BT{}, t_begin + j + 2, j + 2 < nt, t_begin + j + 1, true);
       }
       if constexpr (P == 0)
-        phase_b(I0{}, hs_, pa, pb);
+        phase_b(I0{}, hs_, pa, pb, t_begin + j + 1, j + 1 < nt);
       else
-        phase_b(I1{}, hs_, pb, pa);
+        phase_b(I1{}, hs_, pb, pa, t_begin + j + 1, j + 1 < nt);
       ATTN_TILE_SYNC();
     };
     if (nt > 0) {
@@ -705,18 +718,25 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     }
   }
 
-  if (q_row >= q_len) return;
+  if (q_row >= q_len) return;  // lanes l and l + 32 hold the same row: the pairs below stay whole
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
   bf16_t* orow = p.o + (long)(q_start + q_row) * p.o_row_stride + (long)h * p.o_head_stride;
+  // Lane (row, hh) holds columns i*32 + 8*r4 + 4*hh + 0..3. For each pair (r4, r4 + 1) one v_permlane32_swap per
+  // dword gives the lower half-wave columns 16*rp + 0..7 and the upper half 16*rp + 8..15: one 16-B store per
+  // pair instead of two 8-B stores (the store tail is issue-bound; MI355X guide T21).
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
-    for (int r4 = 0; r4 < 4; ++r4) {
-      const int d = i * 32 + 8 * r4 + 4 * hh;
-      u32x2 w;
-      w.x = pack2bf(o_acc[i][4 * r4 + 0] * inv, o_acc[i][4 * r4 + 1] * inv);
-      w.y = pack2bf(o_acc[i][4 * r4 + 2] * inv, o_acc[i][4 * r4 + 3] * inv);
-      *(u32x2*)(orow + d) = w;
+    for (int rp = 0; rp < 2; ++rp) {
+      const int ra = 8 * rp, rb = 8 * rp + 4;
+      unsigned a0 = pack2bf(o_acc[i][ra + 0] * inv, o_acc[i][ra + 1] * inv);
+      unsigned a1 = pack2bf(o_acc[i][ra + 2] * inv, o_acc[i][ra + 3] * inv);
+      unsigned b0 = pack2bf(o_acc[i][rb + 0] * inv, o_acc[i][rb + 1] * inv);
+      unsigned b1 = pack2bf(o_acc[i][rb + 2] * inv, o_acc[i][rb + 3] * inv);
+      const auto x0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto x1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      const u32x4 w = {x0[0], x1[0], x0[1], x1[1]};
+      *(u32x4*)(orow + i * 32 + 16 * rp + 8 * hh) = w;
     }
   }
   ATTN_STAMP(2);
