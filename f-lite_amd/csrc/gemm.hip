@@ -464,9 +464,12 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-// linear tile id -> (m0, n0): groups of 8 M-tiles, M-fastest inside a group (L2 reuse of W columns)
+// linear tile id -> (m0, n0): groups of GEMM_GROUP M-tiles, M-fastest inside a group (L2 reuse of W columns)
 __device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0, int& n0) {
-  constexpr int GROUP = 8;
+#ifndef GEMM_GROUP
+#define GEMM_GROUP 6  // kbench_gemm A/B on MI355X: 4-6 beat 8 by 1.5-2.5 % (gate/up, 8192^3), 2 and 16 lose
+#endif
+  constexpr int GROUP = GEMM_GROUP;
   const int group_size = GROUP * num_n;
   const int gid = L / group_size;
   const int first_m = gid * GROUP;
