@@ -107,8 +107,12 @@ constexpr int SG_MFMA = 0x008, SG_DSR = 0x100;
 // with tap = ky*3+kx. Each 64-wide k-tile is one tap and 64 consecutive channels (128 contiguous bytes of
 // one input pixel); the buffer range check returns 0 for the padding pixels.
 // `upsample` folds nearest-2x interpolation into the addressing (Upsample2D + conv).
-template <int EPI, bool CONV>
+// MI = 16-row MFMA blocks per wave along M: 8 -> 256-row output tiles, 7 -> 224-row tiles (fewer, smaller
+// tiles where 256 rows leave a last wave of tiles mostly empty; the A staging still copies 256 rows).
+template <int EPI, bool CONV, int MI = 8>
 struct GemmCta {
+  static constexpr int WM = MI * 16;  // output rows per wave_m
+  static constexpr int BMV = 2 * WM;  // output rows per tile
   const GemmParams& p;
   int tid, lane, wave, wave_m, wave_n, lr, lk;
   unsigned lds0;
@@ -139,7 +143,7 @@ struct GemmCta {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const unsigned coff = ((4 * s + lk) ^ swz(lr)) << 4;
-      ab[s] = lds0 + (wave_m * 128 + lr) * 128 + coff;
+      ab[s] = lds0 + (wave_m * WM + lr) * 128 + coff;
       wb[s] = lds0 + W_REGION + (wave_n * 64 + lr) * 128 + coff;
     }
   }
@@ -228,18 +232,19 @@ struct GemmCta {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
-        acc[mi0 + i][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[i], acc[mi0 + i][ni], 0, 0, 0);
+        if (mi0 + i < MI)
+          acc[mi0 + i][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[i], acc[mi0 + i][ni], 0, 0, 0);
   }
-  // spread NR ds_reads over a half-step's 16 MFMAs
-  template <int NR>
+  // spread NR ds_reads over a half-step's NM MFMAs
+  template <int NR, int NM = 16>
   __device__ __forceinline__ static void interleave() {
-    constexpr int per = 16 / NR;
+    constexpr int per = NM / NR;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       __builtin_amdgcn_sched_group_barrier(SG_MFMA, per, 0);
       __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(SG_MFMA, 16 - per * NR, 0);
+    __builtin_amdgcn_sched_group_barrier(SG_MFMA, NM - per * NR, 0);
   }
 
   // One 64-deep k-tile from LDS buffer BUF. Register sets: wx / wy = W fragments of alternating k-steps,
@@ -262,7 +267,7 @@ struct GemmCta {
 #pragma unroll
     for (int i = 0; i < 4; ++i) al[i] = rd_a<BUF>(1, i);
     mfma_half(acc, wx, ah, 4);
-    interleave<6>();
+    interleave<6, (MI - 4) * 4>();
 #pragma unroll
     for (int i = 0; i < 4; ++i) ah[i] = rd_a<BUF>(1, 4 + i);
     mfma_half(acc, wy, al, 0);
@@ -282,7 +287,7 @@ struct GemmCta {
       al[i] = rd_a<BUF ^ 1>(0, i);
     }
     mfma_half(acc, wy, ah, 4);
-    interleave<8>();
+    interleave<8, (MI - 4) * 4>();
     if constexpr (!CONV) stage(wave_m == 1 ? kt + 2 : ke, BUF);
   }
 
@@ -343,7 +348,7 @@ struct GemmCta {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int m = m_base + (mb + i) * 16;
-        mok[i] = m < p.M;
+        mok[i] = mb + i < MI && m < p.M;
         const int mc = mok[i] ? m : p.M - 1;
         orow[i] = (float*)p.out + (long)mc * p.ldo;
         const float* grow = GATED ? p.gate + (long)(mc / p.rows_per_seg) * p.gate_seg_stride : nullptr;
@@ -373,14 +378,14 @@ struct GemmCta {
 
   // ---- epilogue: lane holds C[m][n..n+3] for m = m_base + mi*16 + (lane&15), n = n_base + ni*16 + 4*(lane>>4)
   __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], int m0, int n0) {
-    const int m_base = m0 + wave_m * 128 + lr;
+    const int m_base = m0 + wave_m * WM + lr;
     const int n_base = n0 + wave_n * 64 + lk * 4;
 
     if constexpr (EPI == EPI_SWIGLU_BF16) {
       // pairs (ni=0 gate, ni=1 up), (ni=2 gate, ni=3 up) -> output column (n0/2 + wave_n*32 + pair*16 + 4*(lane>>4))
       const int F = p.N >> 1;
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
+      for (int mi = 0; mi < MI; ++mi) {
         const int m = m_base + mi * 16;
         if (m >= p.M) continue;
         bf16_t* orow = (bf16_t*)p.out + (long)m * p.ldo;
@@ -413,7 +418,7 @@ struct GemmCta {
           bias[ni][r] = (p.bias != nullptr && n < p.N) ? bf2f(p.bias[n]) : 0.f;
         }
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
+      for (int mi = 0; mi < MI; ++mi) {
         const int m = m_base + mi * 16;
         if (m >= p.M) continue;
         const long om = p.out_seg > 0 ? (m / p.out_seg) * p.out_seg_stride + p.out_seg_off + (m % p.out_seg) : m;
@@ -465,7 +470,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 // linear tile id -> (m0, n0): groups of GEMM_GROUP M-tiles, M-fastest inside a group (L2 reuse of W columns)
-__device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0, int& n0) {
+__device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0, int& n0, int bm = BM) {
 #ifndef GEMM_GROUP
 #define GEMM_GROUP 6  // kbench_gemm A/B on MI355X: 4-6 beat 8 by 1.5-2.5 % (gate/up, 8192^3), 2 and 16 lose
 #endif
@@ -475,7 +480,7 @@ __device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0
   const int first_m = gid * GROUP;
   const int gm = min(num_m - first_m, GROUP);
   const int rem = L - gid * group_size;
-  m0 = (first_m + rem % gm) * BM;
+  m0 = (first_m + rem % gm) * bm;
   n0 = (rem / gm) * BN;
 }
 
@@ -601,23 +606,24 @@ __device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&ac
 
 // One launch: data-parallel (grid = tiles, one output tile per workgroup) or, when the launcher set
 // p.sk_tiles, the persistent stream-K + data-parallel schedule above (grid = one workgroup per CU).
-template <int EPI, bool CONV>
+template <int EPI, bool CONV, int MI>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  GemmCta<EPI, CONV> c(p, smem);
-  const int num_m = (p.M + BM - 1) / BM;
+  using Cta = GemmCta<EPI, CONV, MI>;
+  Cta c(p, smem);
+  const int num_m = (p.M + Cta::BMV - 1) / Cta::BMV;
   const int num_n = (p.N + BN - 1) / BN;
   const int nk = p.K / BK;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   f32x4 acc[8][4];
-  if constexpr (!CONV) {
+  if constexpr (!CONV && MI == 8) {
     if (p.sk_tiles > 0) {
       stream_k_body<EPI>(c, acc, num_m, num_n, nk, wg);
       return;
     }
   }
   int m0, n0;
-  tile_origin(wg, num_m, num_n, m0, n0);
+  tile_origin(wg, num_m, num_n, m0, n0, Cta::BMV);
   c.setup_tile(m0, n0);
   c.mainloop(acc, 0, nk);
   c.epilogue(acc, m0, n0);
@@ -646,17 +652,33 @@ int choose_sk_tiles(const GemmParams& p, int T) {
   return sk < 0.97 * dp ? rem : 0;
 }
 
+// Tile height: 224-row tiles (MI = 7) where they take fewer rounds x tile size than 256-row tiles on the
+// G CUs (e.g. M = 8224, N = 3072: 444 tiles = 2 rounds of 7/8-size tiles instead of 396 = 2 full rounds);
+// stream-K (256-row tiles only) keeps priority where its model takes it.
+bool use_bm224(const GemmParams& p) {
+  if (p.conv_in != nullptr || g_num_cu <= 0) return false;
+  const int G = g_num_cu;
+  const int num_n = (p.N + BN - 1) / BN;
+  const int t256 = (p.M + 255) / 256 * num_n, t224 = (p.M + 223) / 224 * num_n;
+  const double r256 = (double)((t256 + G - 1) / G), r224 = (double)((t224 + G - 1) / G) * 0.875;
+  return r224 < 0.97 * r256;
+}
+
 template <int EPI>
 int launch(GemmParams p, hipStream_t s) {
-  const int num_m = (p.M + BM - 1) / BM;
   const int num_n = (p.N + BN - 1) / BN;
-  const int T = num_m * num_n;
+  const int T = (p.M + BM - 1) / BM * num_n;
   p.sk_tiles = choose_sk_tiles(p, T);
-  const int grid = p.sk_tiles ? g_num_cu : T;
-  if (p.conv_in != nullptr)
-    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true>), dim3(grid), dim3(NT), LDS_BYTES, s, p);
-  else
-    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false>), dim3(grid), dim3(NT), LDS_BYTES, s, p);
+  if (p.conv_in != nullptr) {
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true, 8>), dim3(T), dim3(NT), LDS_BYTES, s, p);
+  } else if (p.sk_tiles) {
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(g_num_cu), dim3(NT), LDS_BYTES, s, p);
+  } else if (use_bm224(p)) {
+    const int T224 = (p.M + 223) / 224 * num_n;
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 7>), dim3(T224), dim3(NT), LDS_BYTES, s, p);
+  } else {
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(T), dim3(NT), LDS_BYTES, s, p);
+  }
   return 0;
 }
 
@@ -664,10 +686,13 @@ bool attrs_done = false;
 
 template <int EPI>
 hipError_t set_attrs() {
-  hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, false>,
+  hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, false, 8>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, false, 7>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          LDS_BYTES);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              LDS_BYTES);
 }
 
@@ -686,7 +711,7 @@ int gemm_init() {
     FLITE_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
     g_num_cu = prop.multiProcessorCount;
     int per_cu = 0;  // the stream-K grid needs every workgroup resident at once
-    FLITE_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_bf16_kernel<EPI_RESID_F32, false>, NT,
+    FLITE_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_bf16_kernel<EPI_RESID_F32, false, 8>, NT,
                                                                 LDS_BYTES));
     if (per_cu < 1) g_num_cu = 0;
   }
