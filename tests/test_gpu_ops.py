@@ -84,6 +84,35 @@ def test_gemm_gated_residual(shared):
     assert rel(x, ref) < 1e-5
 
 
+# 224-row tiles (gemm.hip use_bm224): on 256 CUs, M = 8224 / 8174 with N = 3072 (and 2F = 24576 for SwiGLU) take
+# 2 (14) rounds of 7/8-size tiles instead of 2 (13) full rounds, so the launcher runs MI = 7. Ragged last tiles
+# (8224 = 36 x 224 + 160, 8174 = 36 x 224 + 110) and every epilogue those GEMMs use.
+@pytest.mark.parametrize("M", [8224, 8174])
+def test_gemm_224_row_tiles(M):
+    N, K, T = 3072, 128, 4112
+    g = torch.Generator(device=DEV).manual_seed(M)
+    a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) * 0.05).bfloat16()
+    b = (torch.randn(N, device=DEV, generator=g) * 0.1).bfloat16()
+    y = a.float() @ w.float().t() + b.float()
+    assert rel(nat.gemm(a, w, b), y) < 1e-2
+    assert rel(nat.gemm(a, w, b, epilogue=nat.EPI_STORE_F32), y) < 1e-5
+    nseg = (M + T - 1) // T
+    gate = torch.randn(nseg, N, device=DEV, generator=g)
+    x0 = torch.randn(M, N, device=DEV, generator=g)
+    ref = x0.clone()
+    for s in range(nseg):
+        ref[s * T:(s + 1) * T] += y[s * T:(s + 1) * T] * gate[s]
+    x = x0.clone()
+    nat.gemm(a, w, b, out=x, epilogue=nat.EPI_RESID_F32, gate=gate, gate_seg_stride=N, rows_per_seg=T)
+    assert rel(x, ref) < 1e-5
+    F = 12288
+    wg = (torch.randn(F, K, device=DEV, generator=g) * 0.05).bfloat16()
+    wu = (torch.randn(F, K, device=DEV, generator=g) * 0.05).bfloat16()
+    sw = nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu)
+    assert rel(sw, torch.nn.functional.silu(a.float() @ wg.float().t()) * (a.float() @ wu.float().t())) < 1e-2
+
+
 # Stream-K (flite_gemm_bf16_ws): shapes whose last wave of 256x256 tiles is partial on 256 CUs and whose k-depth
 # makes the split pay (gemm.hip choose_sk_tiles), so the launcher cuts that wave's k-iterations evenly over the
 # CUs: the 10B down projection, and small grids where one tile is shared by up to ~28 workgroups (fan-in).
