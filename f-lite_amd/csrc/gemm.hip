@@ -272,8 +272,17 @@ struct GemmCta {
     for (int i = 0; i < 4; ++i) ah[i] = rd_a<BUF>(1, 4 + i);
     mfma_half(acc, wy, al, 0);
     interleave<4>();
+// GEMM_ABL_*: diagnostic timing builds only (wrong results). On MI355X the DMA wait costs 3.5 % of the gate/up
+// GEMM and 8-11 % of the K = 12288 projections (operands streamed from HBM), nothing at K = 3072, N <= 9216.
+#if defined(GEMM_ABL_NOVMWAIT)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#elif defined(GEMM_ABL_NOSYNC)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+#endif
     // The two waves of a SIMD (w, w + 4) issue their copies of tile t+2 a half-step apart, so one of them
     // keeps the MFMA pipe fed while the other spends issue cycles on LDS-DMA. Not in CONV mode: there the
     // per-tap gather addressing makes the split schedule 1.9x slower (tools/kbench_conv.py).
