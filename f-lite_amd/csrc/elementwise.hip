@@ -113,6 +113,26 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
       v[4 * q + 3] = w[3];
     }
   }
+  // weight, scale and shift (L2-resident, shared by all rows) are loaded before the reduction, so the row's
+  // two memory round trips overlap instead of running back to back
+  const float* shift = p.shift ? p.shift + seg * p.mod_seg_stride : nullptr;
+  const float* scale = p.scale ? p.scale + seg * p.mod_seg_stride : nullptr;
+  float wgt[NQ][4];
+  f32x4 sc[NQ], sh[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int n = q * 1024 + t * 4;
+    wgt[q][0] = wgt[q][1] = wgt[q][2] = wgt[q][3] = 1.f;
+    if (p.w) {
+      const u32x2 ww = *(const u32x2*)(p.w + n);
+      wgt[q][0] = __uint_as_float(ww.x << 16);
+      wgt[q][1] = __uint_as_float(ww.x & 0xffff0000u);
+      wgt[q][2] = __uint_as_float(ww.y << 16);
+      wgt[q][3] = __uint_as_float(ww.y & 0xffff0000u);
+    }
+    sc[q] = scale ? *(const f32x4*)(scale + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    sh[q] = shift ? *(const f32x4*)(shift + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < 4 * NQ; ++i) ss += v[i] * v[i];
@@ -121,26 +141,13 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
   __syncthreads();
   ss = part[0] + part[1] + part[2] + part[3];
   const float r = rsqrtf(ss / (float)(1024 * NQ) + p.eps);
-  const float* shift = p.shift ? p.shift + seg * p.mod_seg_stride : nullptr;
-  const float* scale = p.scale ? p.scale + seg * p.mod_seg_stride : nullptr;
   bf16_t* yr = p.y + m * p.ldy;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int n = q * 1024 + t * 4;
-    float wgt[4] = {1.f, 1.f, 1.f, 1.f};
-    if (p.w) {
-      const u32x2 ww = *(const u32x2*)(p.w + n);
-      wgt[0] = __uint_as_float(ww.x << 16);
-      wgt[1] = __uint_as_float(ww.x & 0xffff0000u);
-      wgt[2] = __uint_as_float(ww.y << 16);
-      wgt[3] = __uint_as_float(ww.y & 0xffff0000u);
-    }
-    f32x4 sc = {0.f, 0.f, 0.f, 0.f}, sh = {0.f, 0.f, 0.f, 0.f};
-    if (scale) sc = *(const f32x4*)(scale + n);
-    if (shift) sh = *(const f32x4*)(shift + n);
     float o[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = v[4 * q + j] * r * wgt[j] * (1.f + sc[j]) + sh[j];
+    for (int j = 0; j < 4; ++j) o[j] = v[4 * q + j] * r * wgt[q][j] * (1.f + sc[q][j]) + sh[q][j];
     u32x2 st;
     st.x = pack2bf(o[0], o[1]);
     st.y = pack2bf(o[2], o[3]);
