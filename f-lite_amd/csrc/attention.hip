@@ -497,7 +497,13 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
           mfma_s(s1, k1[s], qf[s]);
         }
         __builtin_amdgcn_sched_barrier(0);
+// FLITE_ATTN_ABL_*: diagnostic timing builds (wrong outputs). Prices on MI355X at T = 4096 (405 us): the DMA
+// copies 9 %, the V transposed reads 9 %, the softmax 0 % (hidden), the tile barrier 0 %.
+#ifdef FLITE_ATTN_ABL_NODMA
+        if constexpr (false) {
+#else
         if constexpr (DMA) {  // K pieces first (needed first), then V
+#endif
           if (s < 8)
             blds16(krs, k_src[s], lds0 + DKB * TILE + (wave * 8 + s) * 1024 + K_OFF);
           else if (!ATTN_VDMA_B)
@@ -511,7 +517,11 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     auto softmax_elem = [&](u32x4 (&pn)[4], int e, float& e_prev) {
       const f32x16& sacc = e < 16 ? s0 : s1;
       const int r = e & 15;
+#ifdef FLITE_ATTN_ABL_NOEXP
+      const float v = sacc[r] * sl2 - m_run;
+#else
       const float v = __builtin_amdgcn_exp2f(sacc[r] * sl2 - m_run);
+#endif
       l_run += v;
       if (e & 1) {
         const bf16x2 pr = {(__bf16)e_prev, (__bf16)v};
@@ -530,8 +540,13 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       s16x4 lo[32], hi[32];
       auto rd = [&](int m) {
         const int g = m >> 3, dt = m & 7, kh = g >> 1, s = g & 1;
+#ifdef FLITE_ATTN_ABL_NOTR
+        lo[m] = s16x4{(short)kh, (short)s, (short)dt, 1};
+        hi[m] = lo[m];
+#else
         lo[m] = ds_tr16(Vb + (kh * 32 + 16 * s) * 512 + v_off[dt]);
         hi[m] = ds_tr16(Vb + (kh * 32 + 16 * s + 8) * 512 + v_off[dt]);
+#endif
       };
 #pragma unroll
       for (int m = 0; m < ATTN_VAHEAD; ++m) rd(m);
