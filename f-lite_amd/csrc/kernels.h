@@ -140,9 +140,13 @@ namespace flite {
 // VAE decoder helpers (vae.hip)
 int group_norm(const bf16_t* x, bf16_t* y, long rows, int C, int G, const bf16_t* gamma, const bf16_t* beta,
                float eps, bool silu, double* stats, hipStream_t s);
-int softmax_rows(const float* S, bf16_t* P, int R, int L, float scale, hipStream_t s);
-int transpose_bf16(const bf16_t* x, bf16_t* y, int R, int C, hipStream_t s);
-int latent_to_nhwc(const float* z, bf16_t* x, int C, int Cpad, int hw, float scaling, float shift, hipStream_t s);
+int softmax_rows(const float* S, bf16_t* P, int R, int L, int ld, float scale, hipStream_t s);
+int transpose_bf16(const bf16_t* x, bf16_t* y, int R, int C, int ldy, hipStream_t s);
+int latent_to_nhwc(const float* z, long plane, int ldz, int th, int tw, bf16_t* x, int C, int Cpad, float scaling,
+                   float shift, hipStream_t s);
+int tile_blend(const float* a, int a_h, int a_w, float* b, int b_h, int b_w, int e, bool vertical, hipStream_t s);
+int tile_to_uint8(const float* t, int tw, unsigned char* img, int img_w, int y0, int x0, int rows, int cols,
+                  hipStream_t s);
 int to_uint8(const float* o, int ld, unsigned char* img, long hw, hipStream_t s);
 int pack_conv_weight(const bf16_t* w, bf16_t* o, int Cout, int Cin, int Cpad, hipStream_t s);
 }  // namespace flite

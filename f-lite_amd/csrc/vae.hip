@@ -3,6 +3,8 @@
 // mid-block attention matmuls run on the MFMA GEMM (gemm.hip, implicit-GEMM conv mode).
 #include <math.h>
 
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -10,15 +12,11 @@ namespace flite {
 
 namespace {
 
-// GroupNorm statistics: sum / sum of squares per group (double accumulation), NHWC rows of C channels.
-// Each thread reads 8 channels (16 B); groups hold C/32 channels (4, 8 or 16).
-__global__ __launch_bounds__(256) void gn_stats_kernel(const bf16_t* x, long rows, int C, int G, double* stats) {
-  __shared__ float s_sum[64], s_sq[64];
-  if (threadIdx.x < 64) {
-    s_sum[threadIdx.x] = 0.f;
-    s_sq[threadIdx.x] = 0.f;
-  }
-  __syncthreads();
+// GroupNorm statistics, pass 1: per-workgroup sum / sum of squares per group into partial[block][G][2], NHWC
+// rows of C channels. Each thread reads 8 channels (16 B); groups hold C/G channels (4, 8 or 16). Every sum
+// runs in a fixed order (no atomics), so the decode is bit-reproducible.
+__global__ __launch_bounds__(256) void gn_stats_kernel(const bf16_t* x, long rows, int C, int G, float* partial) {
+  __shared__ float ps[256][4];
   const int cg = C / G;  // channels per group
   const int vec_per_row = C / 8;
   const long total = rows * vec_per_row;
@@ -47,17 +45,42 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const bf16_t* x, long row
       lq[gi] += f[j] * f[j];
     }
   }
-  atomicAdd(&s_sum[g0], ls[0]);
-  atomicAdd(&s_sq[g0], lq[0]);
-  if (cg < 8) {
-    atomicAdd(&s_sum[g0 + 1], ls[1]);
-    atomicAdd(&s_sq[g0 + 1], lq[1]);
-  }
+  (void)g0;
+  ps[threadIdx.x][0] = ls[0];
+  ps[threadIdx.x][1] = lq[0];
+  ps[threadIdx.x][2] = ls[1];
+  ps[threadIdx.x][3] = lq[1];
   __syncthreads();
-  if (threadIdx.x < G) {
-    atomicAdd(&stats[2 * threadIdx.x], (double)s_sum[threadIdx.x]);
-    atomicAdd(&stats[2 * threadIdx.x + 1], (double)s_sq[threadIdx.x]);
+  // thread u's vectors sit at channel (u % vec_per_row) * 8 (the grid stride is a multiple of vec_per_row)
+  if ((int)threadIdx.x < G) {
+    const int g = threadIdx.x;
+    float s = 0.f, q = 0.f;
+    for (int u = 0; u < 256; ++u) {
+      const int gu = (u % vec_per_row) * 8 / cg;
+      if (gu == g) {
+        s += ps[u][0];
+        q += ps[u][1];
+      } else if (cg < 8 && gu + 1 == g) {
+        s += ps[u][2];
+        q += ps[u][3];
+      }
+    }
+    partial[((long)blockIdx.x * G + g) * 2] = s;
+    partial[((long)blockIdx.x * G + g) * 2 + 1] = q;
   }
+}
+
+// GroupNorm statistics, pass 2: stats[g] = (sum, sum of squares) over the workgroups' partials, in block order
+__global__ __launch_bounds__(64) void gn_finalize_kernel(const float* partial, int nblocks, int G, double* stats) {
+  const int g = threadIdx.x;
+  if (g >= G) return;
+  double s = 0.0, q = 0.0;
+  for (int b = 0; b < nblocks; ++b) {
+    s += (double)partial[((long)b * G + g) * 2];
+    q += (double)partial[((long)b * G + g) * 2 + 1];
+  }
+  stats[2 * g] = s;
+  stats[2 * g + 1] = q;
 }
 
 template <bool SILU>
@@ -99,15 +122,18 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16_t* x, bf16_t* 
   }
 }
 
-// row softmax: P[r][:] = softmax(scale * S[r][:]) (fp32 in, bf16 out), one workgroup per row
-__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* S, bf16_t* P, int L, float scale) {
+// row softmax: P[r][:L] = softmax(scale * S[r][:L]) (fp32 in, bf16 out), P[r][L:ld] = 0 (the zero padding of
+// the P.V GEMM's k dimension); rows of ld (a multiple of 4) elements, one workgroup per row
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* S, bf16_t* P, int L, int ld, float scale) {
   __shared__ float red[8];
-  const float* s = S + (long)blockIdx.x * L;
-  bf16_t* pr = P + (long)blockIdx.x * L;
+  const float* s = S + (long)blockIdx.x * ld;
+  bf16_t* pr = P + (long)blockIdx.x * ld;
   float m = -INFINITY;
-  for (int i = threadIdx.x * 4; i < L; i += 1024) {
+  for (int i = threadIdx.x * 4; i < ld; i += 1024) {
     const f32x4 v = *(const f32x4*)(s + i);
-    m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (i + j < L) m = fmaxf(m, v[j]);
   }
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -115,26 +141,30 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(const float* S, bf16_
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) * scale;
   __syncthreads();
   float sum = 0.f;
-  for (int i = threadIdx.x * 4; i < L; i += 1024) {
+  for (int i = threadIdx.x * 4; i < ld; i += 1024) {
     const f32x4 v = *(const f32x4*)(s + i);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sum += __expf(v[j] * scale - m);
+    for (int j = 0; j < 4; ++j)
+      if (i + j < L) sum += __expf(v[j] * scale - m);
   }
   sum = wave_sum(sum);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
   __syncthreads();
   const float inv = 1.f / (red[0] + red[1] + red[2] + red[3]);
-  for (int i = threadIdx.x * 4; i < L; i += 1024) {
+  for (int i = threadIdx.x * 4; i < ld; i += 1024) {
     const f32x4 v = *(const f32x4*)(s + i);
+    float e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = i + j < L ? __expf(v[j] * scale - m) * inv : 0.f;
     u32x2 w;
-    w.x = pack2bf(__expf(v[0] * scale - m) * inv, __expf(v[1] * scale - m) * inv);
-    w.y = pack2bf(__expf(v[2] * scale - m) * inv, __expf(v[3] * scale - m) * inv);
+    w.x = pack2bf(e[0], e[1]);
+    w.y = pack2bf(e[2], e[3]);
     *(u32x2*)(pr + i) = w;
   }
 }
 
-// bf16 transpose [R, C] -> [C, R] through a 64x64 LDS tile
-__global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* x, bf16_t* y, int R, int C) {
+// bf16 transpose [R, C] -> [C, ldy] (columns R..ldy-1 untouched) through a 64x64 LDS tile
+__global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* x, bf16_t* y, int R, int C, int ldy) {
   __shared__ bf16_t t[64][65];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
@@ -144,18 +174,55 @@ __global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* x, bf16_t*
   __syncthreads();
   for (int i = threadIdx.x; i < 64 * 64; i += 256) {
     const int c = i / 64, r = i % 64;
-    if (r0 + r < R && c0 + c < C) y[(long)(c0 + c) * R + r0 + r] = t[r][c];
+    if (r0 + r < R && c0 + c < C) y[(long)(c0 + c) * ldy + r0 + r] = t[r][c];
   }
 }
 
-// latents (fp32 [C, h, w] of one image) -> NHWC bf16 [h*w, Cpad]: z / scaling + shift (pipeline.py:304)
-__global__ __launch_bounds__(256) void latent_to_nhwc_kernel(const float* z, bf16_t* x, int C, int Cpad, int hw,
-                                                             float inv_scale, float shift) {
-  const long total = (long)hw * Cpad;
+// latents (fp32, channel planes of `plane` elements, rows of `ldz`) -> NHWC bf16 [th*tw, Cpad] of the th x tw
+// window at z: z / scaling + shift (pipeline.py:304). The whole image is the window with ldz = tw.
+__global__ __launch_bounds__(256) void latent_to_nhwc_kernel(const float* z, long plane, int ldz, int tw, long hw,
+                                                             bf16_t* x, int C, int Cpad, float inv_scale,
+                                                             float shift) {
+  const long total = hw * Cpad;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % Cpad);
     const long p = i / Cpad;
-    x[i] = c < C ? f2bf(z[(long)c * hw + p] * inv_scale + shift) : (bf16_t)0;
+    const long y = p / tw, xx = p - y * tw;
+    x[i] = c < C ? f2bf(z[(long)c * plane + y * ldz + xx] * inv_scale + shift) : (bf16_t)0;
+  }
+}
+
+// Tiled decode (diffusers AutoencoderKL.tiled_decode, enabled by the reference at generate.py:77-78): blend the
+// first e rows (vertical) or columns of decoded tile b with the last e of its upper / left neighbour a, in place:
+// b = a * (1 - t/e) + b * (t/e) (AutoencoderKL.blend_v / blend_h). Tiles are fp32 [h][w][4].
+__global__ __launch_bounds__(256) void tile_blend_kernel(const float* a, int a_h, int a_w, float* b, int b_w, int rows,
+                                                         int cols, int e, int vertical) {
+  const long total = (long)rows * cols * 4;
+  const float inv_e = 1.0f / (float)e;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i & 3);
+    const long q = i >> 2;
+    const int y = (int)(q / cols), x = (int)(q - (long)y * cols);
+    const float t = (float)(vertical ? y : x) * inv_e;
+    const long ai = vertical ? ((long)(a_h - e + y) * a_w + x) : ((long)y * a_w + (a_w - e + x));
+    float& bv = b[((long)y * b_w + x) * 4 + c];
+    bv = a[ai * 4 + c] * (1.f - t) + bv * t;
+  }
+}
+
+// the uint8 post-processing (pipeline.py:324-326) of the rows x cols top-left crop of a decoded tile
+// (fp32 [.][tw][4]) into the image (uint8 [.][img_w][3]) at (y0, x0)
+__global__ __launch_bounds__(256) void tile_to_uint8_kernel(const float* t, int tw, unsigned char* img, int img_w,
+                                                            int y0, int x0, int rows, int cols) {
+  const long total = (long)rows * cols * 3;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / 3;
+    const int c = (int)(i - p * 3);
+    const int y = (int)(p / cols), x = (int)(p - (long)y * cols);
+    float v = t[((long)y * tw + x) * 4 + c] * 0.5f + 0.5f;
+    v = fminf(fmaxf(v, 0.f), 1.f) * 255.f;
+    v = rintf(v);
+    img[((long)(y0 + y) * img_w + x0 + x) * 3 + c] = (unsigned char)fminf(fmaxf(v, 0.f), 255.f);
   }
 }
 
@@ -195,12 +262,14 @@ int group_norm(const bf16_t* x, bf16_t* y, long rows, int C, int G, const bf16_t
                float eps, bool silu, double* stats, hipStream_t s) {
   FLITE_REQUIRE(C % G == 0 && C % 8 == 0 && C / G >= 4 && (C / G) % 4 == 0, "group_norm: unsupported channels");
   FLITE_REQUIRE(G <= 64, "group_norm: at most 64 groups");
-  FLITE_HIP_CHECK(hipMemsetAsync(stats, 0, 2 * G * sizeof(double), s));
   const long vecs = rows * (C / 8);
   // the grid stride (blocks * 256) must be a multiple of C/8 so that each thread stays on one channel vector
   FLITE_REQUIRE(256 % (C / 8) == 0, "group_norm: C/8 must divide 256");
   const int blocks = std::min(1024, grid_of(vecs));
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(blocks), dim3(256), 0, s, x, rows, C, G, stats);
+  // workspace: stats double[2 * 64], then the per-workgroup partials float[1024][64][2]
+  float* partial = (float*)(stats + 2 * 64);
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(blocks), dim3(256), 0, s, x, rows, C, G, partial);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(1), dim3(64), 0, s, partial, blocks, G, stats);
   if (silu)
     hipLaunchKernelGGL(gn_apply_kernel<true>, dim3(grid_of(vecs)), dim3(256), 0, s, x, y, rows, C, G, stats, gamma,
                        beta, eps);
@@ -211,22 +280,43 @@ int group_norm(const bf16_t* x, bf16_t* y, long rows, int C, int G, const bf16_t
   return 0;
 }
 
-int softmax_rows(const float* S, bf16_t* P, int R, int L, float scale, hipStream_t s) {
-  FLITE_REQUIRE(L % 4 == 0, "softmax_rows: L must be a multiple of 4");
-  hipLaunchKernelGGL(softmax_rows_kernel, dim3(R), dim3(256), 0, s, S, P, L, scale);
+int softmax_rows(const float* S, bf16_t* P, int R, int L, int ld, float scale, hipStream_t s) {
+  FLITE_REQUIRE(ld % 4 == 0 && ld >= L, "softmax_rows: ld must be a multiple of 4 and >= L");
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3(R), dim3(256), 0, s, S, P, L, ld, scale);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }
 
-int transpose_bf16(const bf16_t* x, bf16_t* y, int R, int C, hipStream_t s) {
-  hipLaunchKernelGGL(transpose_kernel, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, s, x, y, R, C);
+int transpose_bf16(const bf16_t* x, bf16_t* y, int R, int C, int ldy, hipStream_t s) {
+  FLITE_REQUIRE(ldy >= R, "transpose_bf16: ldy must be >= R");
+  hipLaunchKernelGGL(transpose_kernel, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, s, x, y, R, C, ldy);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }
 
-int latent_to_nhwc(const float* z, bf16_t* x, int C, int Cpad, int hw, float scaling, float shift, hipStream_t s) {
-  hipLaunchKernelGGL(latent_to_nhwc_kernel, dim3(grid_of((long)hw * Cpad)), dim3(256), 0, s, z, x, C, Cpad, hw,
-                     1.0f / scaling, shift);
+int latent_to_nhwc(const float* z, long plane, int ldz, int th, int tw, bf16_t* x, int C, int Cpad, float scaling,
+                   float shift, hipStream_t s) {
+  const long hw = (long)th * tw;
+  hipLaunchKernelGGL(latent_to_nhwc_kernel, dim3(grid_of(hw * Cpad)), dim3(256), 0, s, z, plane, ldz, tw, hw, x, C,
+                     Cpad, 1.0f / scaling, shift);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int tile_blend(const float* a, int a_h, int a_w, float* b, int b_h, int b_w, int e, bool vertical, hipStream_t s) {
+  FLITE_REQUIRE(e > 0 && e <= (vertical ? std::min(a_h, b_h) : std::min(a_w, b_w)), "tile_blend: bad extent");
+  FLITE_REQUIRE(vertical ? a_w == b_w : a_h == b_h, "tile_blend: neighbours must share the blended edge");
+  const int rows = vertical ? e : b_h, cols = vertical ? b_w : e;
+  hipLaunchKernelGGL(tile_blend_kernel, dim3(grid_of((long)rows * cols * 4)), dim3(256), 0, s, a, a_h, a_w, b, b_w,
+                     rows, cols, e, vertical ? 1 : 0);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int tile_to_uint8(const float* t, int tw, unsigned char* img, int img_w, int y0, int x0, int rows, int cols,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(tile_to_uint8_kernel, dim3(grid_of((long)rows * cols * 3)), dim3(256), 0, s, t, tw, img, img_w,
+                     y0, x0, rows, cols);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

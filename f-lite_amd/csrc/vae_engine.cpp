@@ -2,6 +2,7 @@
 // block_out_channels (128, 256, 512, 512), layers_per_block 2, 32 groups, mid-block attention), called by the
 // reference at pipeline.py:301-307 after `latents / scaling_factor + shift_factor`, followed by the uint8
 // post-processing of pipeline.py:324-326. NHWC bf16 activations; convs = implicit-GEMM MFMA (gemm.hip).
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -15,7 +16,10 @@ namespace flite {
 class VaeEngine {
  public:
   explicit VaeEngine(const flite_vae_config& c) : cfg(c) {}
-  ~VaeEngine() { free_ws(); }
+  ~VaeEngine() {
+    free_ws();
+    free_tiles();
+  }
 
   int bind(const std::string& name, const void* p, long n) {
     FLITE_REQUIRE(p != nullptr && ((uintptr_t)p & 15) == 0, "vae bind: null or unaligned " + name);
@@ -47,12 +51,13 @@ class VaeEngine {
     maxe = std::max(maxe, H * W * 4);
     for (int i = 0; i < 5; ++i)
       if (alloc((void**)&buf_[i], maxe * 2)) return 1;
-    const long L = (long)h * w;  // mid-block attention tokens
+    const long L = (long)h * w;  // mid-block attention tokens; the P.V k dimension is padded to 64
+    const long Lp = (L + 63) / 64 * 64;
     const int Cm = cfg.block_out_channels[cfg.n_blocks - 1];
-    if (alloc((void**)&S_, L * L * 4)) return 1;
-    if (alloc((void**)&P_, L * L * 2)) return 1;
-    if (alloc((void**)&vt_, L * Cm * 2)) return 1;
-    if (alloc((void**)&stats_, 64 * 2 * sizeof(double))) return 1;
+    if (alloc((void**)&S_, L * Lp * 4)) return 1;
+    if (alloc((void**)&P_, L * Lp * 2)) return 1;
+    if (alloc((void**)&vt_, Lp * Cm * 2)) return 1;
+    if (alloc((void**)&stats_, FLITE_GROUP_NORM_WS_DOUBLES * sizeof(double))) return 1;
     if (alloc((void**)&out32_, H * W * 4 * 4)) return 1;
     return pack_all();
   }
@@ -60,12 +65,94 @@ class VaeEngine {
   // decode one image: z fp32 [C, h, w] -> img uint8 [H, W, 3]
   int decode(hipStream_t s, const float* z, unsigned char* img, float scaling, float shift) {
     FLITE_REQUIRE(h_ > 0, "vae decode: call prepare first");
+    if (decode_core(s, z, (long)h_ * w_, w_, h_, w_, out32_, scaling, shift)) return 1;
+    const long H = (long)h_ << (cfg.n_blocks - 1), W = (long)w_ << (cfg.n_blocks - 1);
+    return to_uint8(out32_, 4, img, H * W, s);
+  }
+
+  // Tiled decode (diffusers AutoencoderKL.tiled_decode; the reference enables it at generate.py:77-78, and
+  // AutoencoderKL.decode takes it when a latent side exceeds tile_latent). Latent tiles of tile_latent start
+  // every stride = int(tile_latent * (1 - overlap)) rows / columns (the last ones smaller); each decodes to an
+  // fp32 tile that is blended in place with its already-blended upper, then left neighbour over
+  // e = int(tile_sample * overlap) pixels, then cropped to tile_sample - e and post-processed into the image.
+  int prepare_tiled(int H, int W, int tile_latent, int tile_sample, float overlap) {
+    FLITE_REQUIRE(H > 0 && W > 0 && tile_latent > 0 && tile_sample == tile_latent << (cfg.n_blocks - 1),
+                  "vae prepare_tiled: tile_sample must be tile_latent x 8");
+    const int stride = (int)(tile_latent * (1.0 - overlap));
+    const int blend = (int)(tile_sample * overlap);
+    FLITE_REQUIRE(stride > 0 && blend > 0 && blend < tile_sample, "vae prepare_tiled: overlap out of range");
+    if (prepare(std::min(H, tile_latent), std::min(W, tile_latent))) return 1;
+    if (H == tH_ && W == tW_ && tile_latent == tl_ && tile_sample == ts_ && stride == tstride_ && !tiles_.empty())
+      return 0;
+    free_tiles();
+    tH_ = H;
+    tW_ = W;
+    tl_ = tile_latent;
+    ts_ = tile_sample;
+    tstride_ = stride;
+    tblend_ = blend;
+    for (int i = 0; i < H; i += stride) ti_.push_back(i);
+    for (int j = 0; j < W; j += stride) tj_.push_back(j);
+    for (int i : ti_)
+      for (int j : tj_) {
+        const long th = std::min(tile_latent, H - i), tw = std::min(tile_latent, W - j);
+        void* p = nullptr;
+        FLITE_HIP_CHECK(hipMalloc(&p, (th << (cfg.n_blocks - 1)) * (tw << (cfg.n_blocks - 1)) * 4 * sizeof(float)));
+        tiles_.push_back((float*)p);
+      }
+    return 0;
+  }
+
+  // one image: z fp32 [C, tH, tW] -> img uint8 [8 tH, 8 tW, 3]
+  int decode_tiled(hipStream_t s, const float* z, unsigned char* img, float scaling, float shift) {
+    FLITE_REQUIRE(!tiles_.empty(), "vae decode_tiled: call prepare_tiled first");
+    const int up = cfg.n_blocks - 1;
+    const int nj = (int)tj_.size();
+    auto th = [&](int a) { return std::min(tl_, tH_ - ti_[a]) << up; };  // decoded tile height (pixels)
+    auto tw = [&](int b) { return std::min(tl_, tW_ - tj_[b]) << up; };
+    for (size_t a = 0; a < ti_.size(); ++a)
+      for (int b = 0; b < nj; ++b)
+        if (decode_core(s, z + (long)ti_[a] * tW_ + tj_[b], (long)tH_ * tW_, tW_, th(a) >> up, tw(b) >> up,
+                        tiles_[a * nj + b], scaling, shift))
+          return 1;
+    const int row_limit = ts_ - tblend_;
+    int y0 = 0;
+    for (size_t a = 0; a < ti_.size(); ++a) {
+      int x0 = 0;
+      for (int b = 0; b < nj; ++b) {
+        float* t = tiles_[a * nj + b];
+        if (a > 0) {
+          const float* u = tiles_[(a - 1) * nj + b];
+          if (tile_blend(u, th(a - 1), tw(b), t, th(a), tw(b), std::min({th(a - 1), th(a), tblend_}), true, s))
+            return 1;
+        }
+        if (b > 0) {
+          const float* l = tiles_[a * nj + b - 1];
+          if (tile_blend(l, th(a), tw(b - 1), t, th(a), tw(b), std::min({tw(b - 1), tw(b), tblend_}), false, s))
+            return 1;
+        }
+        const int rows = std::min(row_limit, th(a)), cols = std::min(row_limit, tw(b));
+        if (tile_to_uint8(t, tw(b), img, tW_ << up, y0, x0, rows, cols, s)) return 1;
+        x0 += cols;
+      }
+      y0 += std::min(row_limit, th(a));
+    }
+    return 0;
+  }
+
+  // the decoder network on the th x tw latent window at z (channel planes of `plane`, rows of `ldz`) ->
+  // conv_out fp32 [8th * 8tw, 4] in out
+  int decode_core(hipStream_t s, const float* z, long plane, int ldz, int th, int tw, float* out, float scaling,
+                  float shift) {
+    FLITE_REQUIRE(th > 0 && tw > 0 && (long)th * tw <= (long)h_ * w_ && th <= std::max(h_, w_) &&
+                      tw <= std::max(h_, w_),
+                  "vae decode: window larger than the prepared size");
     const int C0 = cfg.latent_channels;
     const int G = cfg.norm_groups;
-    long h = h_, w = w_;
+    long h = th, w = tw;
     const int Cm = cfg.block_out_channels[cfg.n_blocks - 1];
     bf16_t* x = buf_[0];
-    if (latent_to_nhwc(z, buf_[4], C0, 64, (int)(h * w), scaling, shift, s)) return 1;
+    if (latent_to_nhwc(z, plane, ldz, th, tw, buf_[4], C0, 64, scaling, shift, s)) return 1;
     if (conv3(s, buf_[4], 64, h, w, false, "decoder.conv_in", Cm, x, nullptr)) return 1;
     int cur = 0;
     int C = Cm;
@@ -97,17 +184,19 @@ class VaeEngine {
     {
       GemmParams g;
       if (conv_params(g, buf_[t], C, h, w, false, "decoder.conv_out", 3)) return 1;
-      g.out = out32_;
+      g.out = out;
       g.ldo = 4;
       if (gemm_bf16(g, EPI_STORE_F32, s)) return 1;
     }
     (void)G;
-    return to_uint8(out32_, 4, img, h * w, s);
+    return 0;
   }
 
   const flite_vae_config cfg;
   long latent_elems() const { return (long)cfg.latent_channels * h_ * w_; }
   long image_bytes() const { return 3L * ((long)h_ << (cfg.n_blocks - 1)) * ((long)w_ << (cfg.n_blocks - 1)); }
+  long tiled_latent_elems() const { return (long)cfg.latent_channels * tH_ * tW_; }
+  long tiled_image_bytes() const { return 3L * ((long)tH_ << (cfg.n_blocks - 1)) * ((long)tW_ << (cfg.n_blocks - 1)); }
 
  private:
   struct Param {
@@ -130,6 +219,13 @@ class VaeEngine {
     allocs_.clear();
     packed_.clear();
     h_ = w_ = 0;
+  }
+  void free_tiles() {
+    for (float* p : tiles_) hipFree(p);
+    tiles_.clear();
+    ti_.clear();
+    tj_.clear();
+    tH_ = tW_ = 0;
   }
 
   // pack every 3x3 conv weight [Cout][Cin][3][3] -> [Cout][3][3][Cin_pad]
@@ -230,6 +326,7 @@ class VaeEngine {
   // diffusers Attention (heads 1, dim_head C, residual_connection, group_norm): in place on buf_[cur]
   int attention(hipStream_t s, const std::string& pre, int& cur, int C, long h, long w) {
     const long L = h * w;
+    const long Lp = (L + 63) / 64 * 64;
     const int a = (cur + 1) % 4, qb = (cur + 2) % 4, kb = (cur + 3) % 4;
     bf16_t* x = buf_[cur];
     if (gn(s, x, buf_[a], L, C, pre + ".group_norm", false)) return 1;
@@ -260,25 +357,27 @@ class VaeEngine {
       g.W = buf_[kb];
       g.ldw = C;
       g.out = S_;
-      g.ldo = L;
+      g.ldo = Lp;
       g.M = (int)L;
       g.N = (int)L;
       g.K = C;
       if (gemm_bf16(g, EPI_STORE_F32, s)) return 1;
     }
-    if (softmax_rows(S_, P_, (int)L, (int)L, 1.0f / sqrtf((float)C), s)) return 1;
-    if (transpose_bf16(v, vt_, (int)L, C, s)) return 1;
+    // P [L, Lp] and V^T [C, Lp] with zero columns L..Lp-1: the P.V GEMM runs over k = Lp (a multiple of 64)
+    if (softmax_rows(S_, P_, (int)L, (int)L, (int)Lp, 1.0f / sqrtf((float)C), s)) return 1;
+    if (Lp != L) FLITE_HIP_CHECK(hipMemsetAsync(vt_, 0, (size_t)C * Lp * 2, s));
+    if (transpose_bf16(v, vt_, (int)L, C, (int)Lp, s)) return 1;
     {  // O = P V
       GemmParams g;
       g.A = P_;
-      g.lda = L;
+      g.lda = Lp;
       g.W = vt_;
-      g.ldw = L;
+      g.ldw = Lp;
       g.out = buf_[qb];
       g.ldo = C;
       g.M = (int)L;
       g.N = C;
-      g.K = (int)L;
+      g.K = (int)Lp;
       if (gemm_bf16(g, EPI_STORE_BF16, s)) return 1;
     }
     // to_out[0] + residual (rescale_output_factor 1)
@@ -297,6 +396,10 @@ class VaeEngine {
   bf16_t* vt_ = nullptr;
   double* stats_ = nullptr;
   float* out32_ = nullptr;
+  // tiled decode: latent size, tile geometry, tile origins, decoded fp32 tiles (row-major over the grid)
+  int tH_ = 0, tW_ = 0, tl_ = 0, ts_ = 0, tstride_ = 0, tblend_ = 0;
+  std::vector<int> ti_, tj_;
+  std::vector<float*> tiles_;
 };
 
 }  // namespace flite
@@ -336,6 +439,26 @@ int flite_vae_bind(flite_vae* v, const char* name, const void* ptr, long numel) 
 int flite_vae_prepare(flite_vae* v, int latent_h, int latent_w) {
   FLITE_REQUIRE(v, "flite_vae_prepare: null engine");
   return v->eng->prepare(latent_h, latent_w);
+}
+
+int flite_vae_prepare_tiled(flite_vae* v, int latent_h, int latent_w, int tile_latent, int tile_sample,
+                            float overlap_factor) {
+  FLITE_REQUIRE(v, "flite_vae_prepare_tiled: null engine");
+  return v->eng->prepare_tiled(latent_h, latent_w, tile_latent, tile_sample, overlap_factor);
+}
+
+int flite_vae_decode_tiled_uint8(flite_vae* v, void* stream, const float* latents, int n_img, void* images,
+                                 float scaling_factor, float shift_factor) {
+  FLITE_REQUIRE(v && latents && images, "flite_vae_decode_tiled_uint8: null argument");
+  const long lat_elems = v->eng->tiled_latent_elems();
+  const long img_bytes = v->eng->tiled_image_bytes();
+  FLITE_REQUIRE(lat_elems > 0, "flite_vae_decode_tiled_uint8: call flite_vae_prepare_tiled first");
+  for (int i = 0; i < n_img; ++i) {  // one image at a time (enable_slicing), each tiled
+    if (v->eng->decode_tiled((hipStream_t)stream, latents + i * lat_elems, (unsigned char*)images + i * img_bytes,
+                             scaling_factor, shift_factor))
+      return 1;
+  }
+  return 0;
 }
 
 int flite_vae_decode_uint8(flite_vae* v, void* stream, const float* latents, int n_img, void* images,

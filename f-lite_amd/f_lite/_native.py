@@ -81,6 +81,8 @@ SIGNATURES = {
     "flite_vae_bind": (_i, [_vp, _cp, _vp, _l]),
     "flite_vae_prepare": (_i, [_vp, _i, _i]),
     "flite_vae_decode_uint8": (_i, [_vp, _vp, _vp, _i, _vp, _f, _f]),
+    "flite_vae_prepare_tiled": (_i, [_vp, _i, _i, _i, _i, _f]),
+    "flite_vae_decode_tiled_uint8": (_i, [_vp, _vp, _vp, _i, _vp, _f, _f]),
     "flite_dit_set_probe": (_i, [_vp, _i, _i]),
     "flite_dit_read_probe": (_i, [_vp, ctypes.POINTER(_f), _i, ctypes.POINTER(_i)]),
 }
@@ -401,6 +403,18 @@ class VaeEngine:
                                               float(scaling), float(shift)), "flite_vae_decode_uint8")
         return img
 
+    def prepare_tiled(self, h, w, tile_latent, tile_sample, overlap):
+        check(self.lib.flite_vae_prepare_tiled(self.h, h, w, int(tile_latent), int(tile_sample), float(overlap)),
+              "flite_vae_prepare_tiled")
+
+    def decode_tiled_uint8(self, z, img, scaling, shift):
+        require_gpu(z, "latents", torch.float32)
+        require_gpu(img, "images", torch.uint8)
+        check(self.lib.flite_vae_decode_tiled_uint8(self.h, stream_ptr(z.device), z.data_ptr(), z.shape[0],
+                                                    img.data_ptr(), float(scaling), float(shift)),
+              "flite_vae_decode_tiled_uint8")
+        return img
+
 
 def conv3x3(x_nhwc, weight, bias=None, upsample=False, resid=None, out_f32=False):
     """nn.Conv2d(k=3, pad=1) (+ nearest-2x upsample first) on NHWC bf16 [h, w, cin]; weight [cout, cin, 3, 3]."""
@@ -421,11 +435,14 @@ def conv3x3(x_nhwc, weight, bias=None, upsample=False, resid=None, out_f32=False
     return out
 
 
+GROUP_NORM_WS_DOUBLES = 2 * 64 + 1024 * 64  # include/flite.h FLITE_GROUP_NORM_WS_DOUBLES
+
+
 def group_norm(x, groups, gamma, beta, eps=1e-6, silu=False):
     lib = load()
     rows, C = x.shape
     y = torch.empty_like(x)
-    stats = torch.empty(2 * groups, device=x.device, dtype=torch.float64)
+    stats = torch.empty(GROUP_NORM_WS_DOUBLES, device=x.device, dtype=torch.float64)
     check(lib.flite_group_norm(stream_ptr(x.device), x.data_ptr(), y.data_ptr(), rows, C, groups, gamma.data_ptr(),
                                beta.data_ptr(), eps, int(silu), stats.data_ptr()), "flite_group_norm")
     return y

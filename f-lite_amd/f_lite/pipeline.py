@@ -103,9 +103,14 @@ class FLitePipeline:
     # ---------------------------------------------------------------- reference API surface
     def enable_vae_slicing(self):
         """pipeline.py:85-88 (the native decoder processes one image at a time already)."""
+        if self.vae is not None and hasattr(self.vae, "enable_slicing"):
+            self.vae.enable_slicing()
 
     def enable_vae_tiling(self):
-        """pipeline.py:90-93 (no-op: at <= 1024^2 the reference decodes untiled)."""
+        """pipeline.py:90-93: diffusers tiled decode once a latent side exceeds sample_size / 8 (e.g. the
+        1344x896 default of generate.py); at <= 1024^2 the decode stays untiled, as in the reference."""
+        if self.vae is not None and hasattr(self.vae, "enable_tiling"):
+            self.vae.enable_tiling()
 
     def enable_model_cpu_offload(self, *a, **k):
         """generate.py:72 (no-op: weights stay resident in the 288 GB HBM)."""

@@ -137,6 +137,28 @@ class AutoencoderKL(nn.Module):
         self._engine = None
         self._bound = None
         self._prepared = None
+        # diffusers AutoencoderKL tiling state (enable_tiling / disable_tiling): tiles of sample_size pixels =
+        # sample_size / 2**(levels-1) latents, overlap factor 0.25
+        self.use_tiling = False
+        self.use_slicing = False
+        self.tile_sample_min_size = int(c["sample_size"])
+        self.tile_latent_min_size = int(c["sample_size"]) >> (len(c["block_out_channels"]) - 1)
+        self.tile_overlap_factor = 0.25
+
+    def enable_tiling(self, use_tiling: bool = True):
+        """diffusers AutoencoderKL.enable_tiling (the reference calls it at generate.py:78)."""
+        self.use_tiling = use_tiling
+
+    def disable_tiling(self):
+        self.enable_tiling(False)
+
+    def enable_slicing(self):
+        """diffusers AutoencoderKL.enable_slicing (generate.py:77): the native decoder already decodes one image
+        at a time."""
+        self.use_slicing = True
+
+    def disable_slicing(self):
+        self.use_slicing = False
 
     @classmethod
     def empty(cls, device="cuda", dtype=torch.bfloat16, **cfg):
@@ -210,10 +232,18 @@ class AutoencoderKL(nn.Module):
         shift = self.config.shift_factor if shift_factor is None else shift_factor
         z = latents.float().contiguous()
         B, C, h, w = z.shape
+        n = len(self.config.block_out_channels) - 1
+        img = torch.empty(B, h << n, w << n, 3, device=z.device, dtype=torch.uint8)
+        tl = self.tile_latent_min_size
+        if self.use_tiling and (h > tl or w > tl):  # AutoencoderKL._decode's tiling condition
+            key = ("tiled", h, w, tl, self.tile_sample_min_size, self.tile_overlap_factor)
+            if self._prepared != key:
+                eng.prepare_tiled(h, w, tl, self.tile_sample_min_size, self.tile_overlap_factor)
+                self._prepared = key
+            eng.decode_tiled_uint8(z, img, scaling, shift)
+            return img
         if self._prepared != (h, w):
             eng.prepare(h, w)
             self._prepared = (h, w)
-        n = len(self.config.block_out_channels) - 1
-        img = torch.empty(B, h << n, w << n, 3, device=z.device, dtype=torch.uint8)
         eng.decode_uint8(z, img, scaling, shift)
         return img

@@ -189,7 +189,10 @@ int flite_conv3x3_pack_weight(void* stream, const void* w, void* packed, int cou
 int flite_conv3x3_bf16(void* stream, const void* x, int batch, int h, int w, int cin, int upsample,
                        const void* w_packed, const void* bias, int cout, void* out, const void* resid,
                        int out_is_f32);
-/* GroupNorm (+SiLU) over NHWC bf16 rows (torch.nn.GroupNorm semantics); stats_workspace: device double[2*groups]. */
+/* GroupNorm (+SiLU) over NHWC bf16 rows (torch.nn.GroupNorm semantics), groups <= 64; stats_workspace: device
+ * double[FLITE_GROUP_NORM_WS_DOUBLES] (group sums and the per-workgroup partials of a fixed-order, atomic-free
+ * reduction: bit-reproducible). */
+#define FLITE_GROUP_NORM_WS_DOUBLES (2 * 64 + 1024 * 64)
 int flite_group_norm(void* stream, const void* x, void* y, long rows, int channels, int groups, const void* gamma,
                      const void* beta, float eps, int silu, double* stats_workspace);
 
@@ -217,6 +220,20 @@ int flite_vae_prepare(flite_vae* vae, int latent_h, int latent_w);
 /* latents fp32 [n_img, C, h, w] -> images uint8 [n_img, 8h, 8w, 3] (device), decoding z/scaling + shift. */
 int flite_vae_decode_uint8(flite_vae* vae, void* stream, const float* latents, int n_img, void* images,
                            float scaling_factor, float shift_factor);
+/*
+ * Tiled decode, diffusers AutoencoderKL.tiled_decode / blend_v / blend_h (the reference turns it on with
+ * pipe.vae.enable_tiling(), generate.py:77-78 / pipeline.py:90-93; AutoencoderKL.decode takes it when a latent
+ * side exceeds tile_latent = sample_size / 8, e.g. the 1344x896 default). Latent tiles of tile_latent every
+ * int(tile_latent * (1 - overlap_factor)); decoded tiles blended with their upper then left neighbour over
+ * int(tile_sample * overlap_factor) pixels (linear ramp), cropped to tile_sample minus that, concatenated, then
+ * post-processed to uint8. The FLUX VAE: tile_latent 128, tile_sample 1024, overlap_factor 0.25. Blending is
+ * in fp32 (diffusers blends in the VAE dtype).
+ */
+int flite_vae_prepare_tiled(flite_vae* vae, int latent_h, int latent_w, int tile_latent, int tile_sample,
+                            float overlap_factor);
+/* latents fp32 [n_img, C, latent_h, latent_w] -> images uint8 [n_img, 8 latent_h, 8 latent_w, 3], tiled. */
+int flite_vae_decode_tiled_uint8(flite_vae* vae, void* stream, const float* latents, int n_img, void* images,
+                                 float scaling_factor, float shift_factor);
 
 /*
  * Launch probe (measurement): bracket every launch of one kernel class with a pair of HIP events on the

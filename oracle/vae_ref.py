@@ -130,3 +130,58 @@ def decode_to_uint8(dec: RefVAEDecoder, latents, scaling=FLUX["scaling_factor"],
     img = (img / 2 + 0.5).clamp(0, 1)
     img = (img * 255).round().clamp(0, 255).to(torch.uint8)
     return img.permute(0, 2, 3, 1).contiguous()
+
+
+def _blend_v(a, b, blend_extent):
+    """diffusers AutoencoderKL.blend_v: b's first rows ramp from a's last rows, in place."""
+    e = min(a.shape[2], b.shape[2], blend_extent)
+    for y in range(e):
+        b[:, :, y, :] = a[:, :, -e + y, :] * (1 - y / e) + b[:, :, y, :] * (y / e)
+    return b
+
+
+def _blend_h(a, b, blend_extent):
+    """diffusers AutoencoderKL.blend_h: b's first columns ramp from a's last columns, in place."""
+    e = min(a.shape[3], b.shape[3], blend_extent)
+    for x in range(e):
+        b[:, :, :, x] = a[:, :, :, -e + x] * (1 - x / e) + b[:, :, :, x] * (x / e)
+    return b
+
+
+def tiled_decode(dec, z, tile_latent=128, tile_sample=1024, overlap=0.25):
+    """diffusers AutoencoderKL.tiled_decode (diffusers is third-party and not vendored; requirements.txt:1 leaves
+    it unpinned), which the reference turns on with pipe.vae.enable_tiling() (generate.py:77-78,
+    pipeline.py:90-93) and AutoencoderKL.decode takes once a latent side exceeds tile_latent. Restated from its
+    published algorithm: latent tiles every int(tile_latent * (1 - overlap)), each decoded on its own; every tile
+    blended in place with its (already blended) upper, then left neighbour over int(tile_sample * overlap)
+    pixels; crops of tile_sample - that extent concatenated. `dec` maps scaled latents [B, C, h, w] to images
+    [B, 3, 8h, 8w]. Parity unpinned against diffusers itself; blending in the decoder's dtype (fp32 here)."""
+    overlap_size = int(tile_latent * (1 - overlap))
+    blend_extent = int(tile_sample * overlap)
+    row_limit = tile_sample - blend_extent
+    rows = []
+    for i in range(0, z.shape[2], overlap_size):
+        row = []
+        for j in range(0, z.shape[3], overlap_size):
+            row.append(dec.decode(z[:, :, i:i + tile_latent, j:j + tile_latent]))
+        rows.append(row)
+    result_rows = []
+    for i, row in enumerate(rows):
+        result_row = []
+        for j, tile in enumerate(row):
+            if i > 0:
+                tile = _blend_v(rows[i - 1][j], tile, blend_extent)
+            if j > 0:
+                tile = _blend_h(row[j - 1], tile, blend_extent)
+            result_row.append(tile[:, :, :row_limit, :row_limit])
+        result_rows.append(torch.cat(result_row, dim=3))
+    return torch.cat(result_rows, dim=2)
+
+
+def tiled_decode_to_uint8(dec, latents, tile_latent=128, tile_sample=1024, overlap=0.25,
+                          scaling=FLUX["scaling_factor"], shift=FLUX["shift_factor"]):
+    """pipeline.py:304-326 with the tiled decode above."""
+    img = tiled_decode(dec, latents / scaling + shift, tile_latent, tile_sample, overlap)
+    img = (img / 2 + 0.5).clamp(0, 1)
+    img = (img * 255).round().clamp(0, 255).to(torch.uint8)
+    return img.permute(0, 2, 3, 1).contiguous()

@@ -77,3 +77,40 @@ def test_vae_decode_uint8(lh, lw):
     p = R.psnr(img.float().cpu(), rimg.float(), peak=255.0)
     print(f"VAE {lh}x{lw} uint8 PSNR vs fp32 oracle: {p:.2f} dB")
     assert p >= 40.0
+
+
+# Tiled decode (diffusers AutoencoderKL.tiled_decode, on in the reference via generate.py:77-78) against the oracle
+# restatement, at a reduced tile size so the oracle stays cheap: tile_latent 16 (128 px), stride 12, 32-px blends,
+# 96-px crops; 20 x 28 latents give a 2 x 3 grid with 8-row and 4-column edge tiles.
+def test_vae_decode_tiled_uint8():
+    from oracle.vae_ref import tiled_decode_to_uint8
+
+    vae = AutoencoderKL.random(seed=0)
+    vae.enable_tiling()
+    vae.tile_latent_min_size, vae.tile_sample_min_size = 16, 128
+    ref = RefVAEDecoder(make_vae_state_dict(seed=0))
+    g = torch.Generator().manual_seed(7)
+    lat = torch.randn(1, 16, 20, 28, generator=g)
+    img = vae.decode_to_uint8(lat.to(DEV))
+    rimg = tiled_decode_to_uint8(ref, lat, tile_latent=16, tile_sample=128)
+    assert img.shape == rimg.shape == (1, 160, 224, 3)
+    p = R.psnr(img.float().cpu(), rimg.float(), peak=255.0)
+    print(f"VAE tiled 20x28 (tile 16) uint8 PSNR vs fp32 oracle: {p:.2f} dB")
+    assert p >= 40.0
+    again = vae.decode_to_uint8(lat.to(DEV))
+    assert torch.equal(img, again)
+    vae.disable_tiling()
+    untiled = vae.decode_to_uint8(lat.to(DEV))
+    assert not torch.equal(img, untiled)  # the tiles see only their own window (mid-block attention is global)
+
+
+def test_vae_decode_tiled_default_grid():
+    # the reference's default generate.py resolution: 1344 x 896 -> latents 112 x 168 > 128: 1 x 2 tiles of
+    # 128 latents (stride 96, 256-px blends, 768-px crops) on the full-size Flux VAE
+    vae = AutoencoderKL.random(seed=0)
+    vae.enable_tiling()
+    lat = torch.randn(1, 16, 112, 168, generator=torch.Generator().manual_seed(3)).to(DEV)
+    img = vae.decode_to_uint8(lat)
+    assert img.shape == (1, 896, 1344, 3)
+    assert torch.equal(img, vae.decode_to_uint8(lat))
+    assert img.float().std().item() > 1.0

@@ -104,3 +104,33 @@ def test_flop_accounting_matches_survey():
     from f_lite.vae import decoder_flops
 
     assert abs(decoder_flops(1024, 1024) / 1e12 - 10.47) < 0.01
+
+
+class _PointwiseDecoder:
+    """Stand-in decoder whose pixel (y, x) depends only on latent (y // 8, x // 8): any correct tiling of it
+    (grid, in-place blends of equal overlaps, crops, concatenation) reproduces the untiled output exactly."""
+
+    def decode(self, z):
+        return z[:, :3].repeat_interleave(8, dim=2).repeat_interleave(8, dim=3) * 0.5
+
+
+@pytest.mark.parametrize("h,w,tl", [(112, 168, 128), (20, 28, 16), (16, 40, 16), (33, 7, 8)])
+def test_vae_tiled_decode_grid_is_exact_for_pointwise_decoder(h, w, tl):
+    from oracle.vae_ref import tiled_decode
+
+    g = torch.Generator().manual_seed(h * w)
+    z = torch.randn(1, 16, h, w, generator=g)
+    dec = _PointwiseDecoder()
+    out = tiled_decode(dec, z, tile_latent=tl, tile_sample=8 * tl, overlap=0.25)
+    assert out.shape == (1, 3, 8 * h, 8 * w)
+    torch.testing.assert_close(out, dec.decode(z), rtol=0, atol=1e-6)
+
+
+def test_vae_tiling_flags():
+    from f_lite.vae import AutoencoderKL
+
+    vae = AutoencoderKL.empty(device="cpu")
+    assert (vae.tile_latent_min_size, vae.tile_sample_min_size, vae.tile_overlap_factor) == (128, 1024, 0.25)
+    assert not vae.use_tiling
+    FLitePipeline(None, vae).enable_vae_tiling()  # pipeline.py:90-93 forwards to the VAE
+    assert vae.use_tiling
