@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--guidance", type=float, default=6.0)
     ap.add_argument("--no-vae", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--vae-tiling", action="store_true",
+                    help="pipe.enable_vae_tiling() as generate.py:77-78 does (tiled decode above 1024 px)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
     args = ap.parse_args()
@@ -138,6 +140,8 @@ def main():
 
         vae = AutoencoderKL.random(seed=0, device=dev)
     pipe = FLitePipeline(model, vae)
+    if args.vae_tiling:
+        pipe.enable_vae_tiling()
 
     # synthetic T5 context [1, 512, 4096] (uniform, std 1), generated on rank 0 and broadcast over RCCL/xGMI
     ctx = torch.empty(1, 512, cfg["cross_attn_input_size"], device=dev, dtype=torch.bfloat16)
@@ -237,7 +241,7 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline_sample(model, cfg, args.height, args.width, args.sample_steps)
 
-    metric = "images/sec @%dx%d, %d steps, F-Lite-%s bf16" % (args.height, args.width, args.sample_steps,
+    metric = "images/sec @%dx%d, %d steps, F-Lite-%s bf16" % (args.width, args.height, args.sample_steps,
                                                               args.model.upper())
     if (args.model, args.height, args.width, args.sample_steps) == ("10b", 1024, 1024, 30):
         metric += "; 1/8 GPU + MFMA util%"  # BASELINE.json's metric string (util in mfma_util_image)
@@ -260,7 +264,7 @@ def main():
             args.width, args.height, args.sample_steps, args.guidance,
             "VAE decode to uint8" if vae is not None else "latents only (no VAE)"),
                    "images_per_gpu_per_step": 1, "cfg_batch": 2, "parallelism": "replica dp%d" % world,
-                   "hipgraph": not args.no_graph},
+                   "hipgraph": not args.no_graph, "vae_tiling": bool(args.vae_tiling)},
         "mfma_util_image": round(f_image * value / world / PEAK_BF16, 4),
         "algorithmic_flops_per_image": f_image,
         "roofline": roofline,

@@ -134,18 +134,20 @@ def test_cpu_model_fails_loudly():
         m(torch.zeros(1, 16, 8, 8), torch.zeros(1, 4, 128), torch.tensor([0.5]))
 
 
-def test_forward_full_width_1024():
-    """Full-size shapes of the metric workload: hidden 3072, 12 heads, 1024^2 latents (T = 4112 tokens per sample),
-    CFG batch 2, a 512-token context and the 10B per-block adaLN layout, cut to depth 1 so the fp32 oracle
-    finishes in seconds. Exercises the production schedules: the self-attention tail split (B*H = 24), the
-    stream-K down projection (K = 12288) and the full-size SwiGLU / qkv GEMMs."""
+@pytest.mark.parametrize("lh,lw", [(128, 128), (112, 168)])
+def test_forward_full_width(lh, lw):
+    """Full-size shapes of the metric workload: hidden 3072, 12 heads, 1024^2 latents (T = 4112 tokens per sample)
+    and the reference's generate.py default 1344x896 (T = 4720), CFG batch 2, a 512-token context and the 10B
+    per-block adaLN layout, cut to depth 1 so the fp32 oracle finishes in seconds. Exercises the production
+    schedules: the self-attention tail split (B*H = 24), the stream-K down projection (K = 12288), the 224-row
+    GEMM tiles and the full-size SwiGLU / qkv GEMMs."""
     import dataclasses
 
     cfg = dict(PRESETS["10b"])
     cfg["depth"] = 1
     m = DiT.random(seed=0, device=DEV, **cfg)
     g = torch.Generator().manual_seed(5)
-    x = torch.randn(2, 16, 128, 128, generator=g).bfloat16()
+    x = torch.randn(2, 16, lh, lw, generator=g).bfloat16()
     ctx = torch.randn(2, 512, 4096, generator=g).bfloat16()
     t = torch.tensor([0.75, 0.75]).bfloat16()
     out = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32)
@@ -155,5 +157,5 @@ def test_forward_full_width_1024():
     with torch.no_grad():
         ref = R.RefDiT.random(ref_cfg, dtype=torch.float32)(x.float(), ctx.float(), None, t)
     p = psnr(out, ref)
-    print(f"full-width depth-1 10B-layout forward at 1024^2: PSNR {p:.2f} dB vs fp32 oracle")
+    print(f"full-width depth-1 10B-layout forward at {8 * lw}x{8 * lh}: PSNR {p:.2f} dB vs fp32 oracle")
     assert p >= 40.0
