@@ -232,6 +232,13 @@ int flite_gather_rows(void* stream, const void* src, void* dst, const int* idx, 
   return gather_rows((const bf16_t*)src, (bf16_t*)dst, idx, n, cols, (hipStream_t)stream);
 }
 
+int flite_cfg_euler(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
+                    float dt, int use_cfg) {
+  FLITE_REQUIRE(acc && cond && (uncond || !use_cfg), "flite_cfg_euler: null argument");
+  FLITE_REQUIRE(n >= 0, "flite_cfg_euler: negative element count");
+  return cfg_euler_nchw(uncond, cond, acc, n, guidance, dt, use_cfg, (hipStream_t)stream);
+}
+
 int flite_dit_forward(flite_dit* dit, void* stream, const void* x, int x_is_bf16, int batch, int t_row0,
                       int t_row_step, void* out, int out_is_bf16) {
   FLITE_REQUIRE(dit && x && out, "flite_dit_forward: null argument");

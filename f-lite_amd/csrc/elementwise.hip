@@ -292,6 +292,24 @@ __global__ __launch_bounds__(256) void cfg_euler_kernel(const float* out, float*
   }
 }
 
+// CFG + Euler over NCHW branch outputs, for the CFG-parallel mode where the uncond and cond branches run on
+// two ranks and their [Bi, C, H, W] outputs are exchanged before the update. The fp32 expressions are those
+// of cfg_euler_kernel, so equal branch outputs give a bit-identical accumulator.
+__global__ __launch_bounds__(256) void cfg_euler_nchw_kernel(const float* u, const float* c, float* acc, long n,
+                                                             float g, float dt, int use_cfg) {
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
+    float v;
+    if (use_cfg) {
+      const float uu = u[idx];
+      const float cc = c[idx];
+      v = uu + g * (cc - uu);
+    } else {
+      v = c[idx];
+    }
+    acc[idx] += dt * v;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Adaptive projected guidance (APG, pipeline.py:276-287) + Euler update. The reference reduces over the
 // WHOLE batch tensor, so one 1024-thread workgroup does the three passes (sums, std, update) in-launch.
@@ -527,6 +545,14 @@ int cfg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, 
               hipStream_t s) {
   hipLaunchKernelGGL(cfg_euler_kernel, dim3(grid_for((long)Bi * C * H * W)), dim3(256), 0, s, out, acc, Bi, C, H,
                      W, P, dup, g, dt);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int cfg_euler_nchw(const float* u, const float* c, float* acc, long n, float g, float dt, int use_cfg,
+                   hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(cfg_euler_nchw_kernel, dim3(grid_for(n)), dim3(256), 0, s, u, c, acc, n, g, dt, use_cfg);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

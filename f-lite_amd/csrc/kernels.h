@@ -115,6 +115,8 @@ int patchify(const void* lat, bool in_bf16, bf16_t* out, int Bi, int C, int H, i
 int fill_registers(float* x, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s);
 int cfg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, int dup, float g, float dt,
               hipStream_t s);
+int cfg_euler_nchw(const float* u, const float* c, float* acc, long n, float g, float dt, int use_cfg,
+                   hipStream_t s);
 int unpatchify(const float* out, void* y, bool out_bf16, int B, int C, int H, int W, int P, hipStream_t s);
 int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, float g, float thr, float dt,
               hipStream_t s);

@@ -73,7 +73,8 @@ SIGNATURES = {
     "flite_dit_set_timesteps": (_i, [_vp, _vp, _vp, _i, _i]),
     "flite_dit_forward": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _i]),
     "flite_dit_sample": (_i, [_vp, _vp, _vp, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _f, _i, _i, _f, _i]),
-    "flite_conv3x3_pack_weight": (_i, [_vp, _vp, _vp, _i, _i, _i]),
+    "flite_cfg_euler": (_i, [_vp, _vp, _vp, _vp, _l, _f, _f, _i]),
+    "flite_conv3x3_pack_weight":(_i, [_vp, _vp, _vp, _i, _i, _i]),
     "flite_conv3x3_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i]),
     "flite_group_norm": (_i, [_vp, _vp, _vp, _l, _i, _i, _vp, _vp, _f, _i, _vp]),
     "flite_vae_create": (_i, [_vp, ctypes.POINTER(_vp)]),
@@ -273,6 +274,24 @@ def init_param_(t: torch.Tensor, name: str, seed: int = 0, std: float = 0.02, on
     check(lib.flite_init_param(stream_ptr(t.device), t.data_ptr(), int(t.dtype == torch.bfloat16), t.numel(),
                                name.encode(), seed, std, int(ones)), "flite_init_param")
     return t
+
+
+def cfg_euler_(acc, uncond, cond, guidance, dt, use_cfg=True):
+    """acc += dt * (u + g (c - u)) in place on fp32 NCHW tensors (pipeline.py:290,296-297); cond only when
+    use_cfg is False."""
+    require_gpu(acc, "acc", torch.float32)
+    require_gpu(cond, "cond", torch.float32)
+    if cond.shape != acc.shape:
+        raise FliteError(f"cfg_euler: cond {tuple(cond.shape)} does not match acc {tuple(acc.shape)}")
+    u_ptr = None
+    if use_cfg:
+        require_gpu(uncond, "uncond", torch.float32)
+        if uncond.shape != acc.shape:
+            raise FliteError(f"cfg_euler: uncond {tuple(uncond.shape)} does not match acc {tuple(acc.shape)}")
+        u_ptr = uncond.data_ptr()
+    check(load().flite_cfg_euler(stream_ptr(acc.device), u_ptr, cond.data_ptr(), acc.data_ptr(), acc.numel(),
+                                 float(guidance), float(dt), int(use_cfg)), "flite_cfg_euler")
+    return acc
 
 
 def gather_rows(src, idx, out=None):

@@ -6,11 +6,14 @@ The reference has no multi-GPU inference; its torch.distribu
 the shared text embedding from rank 0 (RCCL over xGMI with the "nccl" backend), before the denoise loop.
 No per-step communication. With APG enabled the reference's batch-global reductions (pipeline.py:281-285)
 couple images; sharded APG is per image (documented in DESIGN.md).
+
+Second mode, for single-image latency: CFG-parallel, the uncond and cond branches of the
+same image on two ranks with one all-gather of the branch outputs per step (`cfg_parallel_sample`).
 """
 from __future__ import annotations
 
 import os
-from typing import List
+from typing import List, Optional
 
 import torch
 
@@ -32,6 +35,78 @@ def broadcast_context(ctx: torch.Tensor, src: int = 0, group=None) -> torch.Tens
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.broadcast(ctx, src=src, group=group)
     return ctx
+
+
+def exchange_branches(out: torch.Tensor, group=None) -> "List[torch.Tensor]":
+    """All-gather of the per-rank CFG branch outputs: [uncond (rank 0), cond (rank 1)]. With the "nccl"
+    backend (RCCL over xGMI) device tensors move directly; gloo (CPU tests) stages through the host."""
+    import torch.distributed as dist
+
+    staged = out.cpu() if dist.get_backend(group) == "gloo" else out
+    bufs = [torch.empty_like(staged) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(bufs, staged.contiguous(), group=group)
+    return [b.to(out.device) for b in bufs]
+
+
+def cfg_parallel_loop(acc: torch.Tensor, t_list, dt_list, forward_branch, update, group=None) -> torch.Tensor:
+    """The denoise loop of FLitePipeline.__call__ (pipeline.py:250-297) with the CFG pair split over the two
+    ranks of `group`: rank 0 runs the uncond branch, rank 1 the cond branch (the batch order of
+    pipeline.py:264-268). Per step each rank runs forward_branch(acc, step) -> [B, C, h, w] fp32, the two
+    outputs are exchanged (one all-gather of B*C*h*w fp32: 1 MiB per image at 1024^2), and both ranks apply the
+    same update(acc, u, c, dt), so their accumulators stay identical."""
+    import torch.distributed as dist
+
+    if dist.get_world_size(group) != 2:
+        raise ValueError("CFG-parallel sampling needs a group of exactly 2 ranks (uncond, cond)")
+    for i, dt in enumerate(dt_list):
+        u, c = exchange_branches(forward_branch(acc, i), group)
+        update(acc, u, c, dt)
+    return acc
+
+
+def cfg_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Tensor,
+                        negative_prompt_embeds: Optional[torch.Tensor] = None, num_inference_steps: int = 30,
+                        guidance_scale: float = 6.0, alpha: Optional[float] = None, group=None) -> torch.Tensor:
+    """Single-image latency mode: the two CFG branches of the same images run on two GPUs
+    (B = n_img per launch instead of 2 n_img), exchanging their outputs once per step; the native CFG + Euler
+    update (flite_cfg_euler) runs on both ranks. Every rank passes the same latents and embeddings and gets
+    the final fp32 latents [n_img, 16, h, w]. Weights are replicated; the branch context (negative on rank 0,
+    positive on rank 1) feeds the step-invariant cross-attention K/V cache once."""
+    import torch.distributed as dist
+
+    from . import _native
+    from .pipeline import flow_schedule
+
+    if guidance_scale < 1.0:
+        raise ValueError("CFG-parallel sampling needs classifier-free guidance (guidance_scale >= 1)")
+    rank = dist.get_rank(group)
+    eng = dit.engine()
+    dev = dit.device
+    n_img, _, lh, lw = latents.shape
+    pos = prompt_embeds.to(device=dev, dtype=torch.bfloat16)
+    neg = torch.zeros_like(pos) if negative_prompt_embeds is None else \
+        negative_prompt_embeds.to(device=dev, dtype=torch.bfloat16)  # pipeline.py:160-161
+    if neg.shape != pos.shape or pos.shape[0] != n_img:
+        raise ValueError("prompt / negative embeddings must both be [n_img, L, C_ctx]")
+    ctx = (neg if rank == 0 else pos).contiguous()
+    L = ctx.shape[1]
+    sched = flow_schedule(num_inference_steps, lh, lw, alpha)
+    t_list = [t for t, _ in sched]
+    dt_list = [dt for _, dt in sched]
+    eng.prepare(n_img, lh, lw, n_img * L, num_inference_steps)
+    eng.set_context(ctx.reshape(n_img * L, -1), [i * L for i in range(n_img + 1)])
+    # one timestep row per step, shared by the batch (pipeline.py:260,268), as in flite_dit_sample
+    eng.set_timesteps(torch.tensor(t_list, dtype=torch.float32, device=dev), bool(eng.cfg.bf16_timestep_quant))
+    acc = latents.to(device=dev, dtype=torch.bfloat16).float().contiguous()
+    out = torch.empty_like(acc)
+
+    def forward_branch(x, i):
+        return eng.forward(x, out, i, 0)
+
+    def update(x, u, c, dt):
+        _native.cfg_euler_(x, u, c, guidance_scale, dt)
+
+    return cfg_parallel_loop(acc, t_list, dt_list, forward_branch, update, group)
 
 
 def max_over_ranks(seconds: float, device=None, group=None) -> float:

@@ -178,6 +178,14 @@ int flite_dit_forward(flite_dit* dit, void* stream, const void* x, int x_is_bf16
 int flite_dit_sample(flite_dit* dit, void* stream, float* acc, int n_img, int n_steps, const float* t_host,
                      const float* dt_host, float guidance, int use_cfg, int apg, float apg_threshold,
                      int use_graph);
+/*
+ * CFG combine + Euler update of pipeline.py:290,296-297 on NCHW fp32 branch outputs [n elements]:
+ * acc += dt * (use_cfg ? u + g (c - u) : c). Used by the CFG-parallel latency mode, where
+ * the uncond and cond branches of one image run on two ranks and are exchanged before the update; the fp32
+ * arithmetic is that of flite_dit_sample's fused update.
+ */
+int flite_cfg_euler(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
+                    float dt, int use_cfg);
 
 /*
  * 3x3 convolution, padding 1, stride 1 (nn.Conv2d of the diffusers VAE decoder), optionally preceded by a

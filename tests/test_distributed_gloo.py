@@ -32,6 +32,58 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _cfg_parallel_worker(rank, world, port, q):
+    """One rank of the CFG-parallel loop; the branch forward is the fp32 oracle (test infrastructure)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from f_lite.distributed import cfg_parallel_loop
+    from oracle import flite_ref as R
+
+    lat, pos, neg = _cfg_inputs()
+    ref = R.RefDiT.random(R.PRESETS["tiny"], dtype=torch.float32)
+    sched = R.schedule(4, 128, 128)
+    ctx = neg if rank == 0 else pos  # uncond on rank 0 (pipeline.py:266)
+
+    def forward_branch(x, i):
+        return ref(x, ctx, None, torch.tensor([sched[i][0]] * x.shape[0], dtype=torch.float32))
+
+    def update(x, u, c, dt):
+        x += dt * (u + 6.0 * (c - u))
+
+    acc = cfg_parallel_loop(lat.clone(), [t for t, _ in sched], [dt for _, dt in sched], forward_branch, update)
+    q.put((rank, acc))
+    dist.destroy_process_group()
+
+
+def _cfg_inputs():
+    g = torch.Generator().manual_seed(11)
+    lat = torch.randn(1, 16, 16, 16, generator=g)
+    pos = torch.randn(1, 24, 128, generator=g)
+    neg = torch.randn(1, 24, 128, generator=g)
+    return lat, pos, neg
+
+
+def test_cfg_parallel_loop_matches_batched_oracle():
+    """CFG-parallel host logic: 2 ranks, one branch each, one all-gather per step; both
+    ranks end with the same latents, equal to the batched CFG loop of pipeline.py:250-297 (fp32 oracle)."""
+    from oracle import flite_ref as R
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cfg_parallel_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(60)
+    assert torch.equal(res[0], res[1])
+    lat, pos, neg = _cfg_inputs()
+    ref = R.sample(R.RefDiT.random(R.PRESETS["tiny"], dtype=torch.float32), lat, pos, neg, num_steps=4,
+                   guidance_scale=6.0, height=128, width=128, t_dtype=torch.float32, acc_dtype=torch.float32)
+    assert torch.allclose(res[0], ref, rtol=1e-4, atol=1e-4), (res[0] - ref).abs().max()
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharding_and_broadcast(world):
     ctx = mp.get_context("spawn")
