@@ -69,6 +69,8 @@ class FLitePipeline:
         self.vae_scale_factor = 8
         self.return_index = -8
         self._progress_bar_config = {}
+        self._cfg_parallel = False
+        self._cfg_group = None
 
     # ---------------------------------------------------------------- loading
     @classmethod
@@ -111,6 +113,20 @@ class FLitePipeline:
         1344x896 default of generate.py); at <= 1024^2 the decode stays untiled, as in the reference."""
         if self.vae is not None and hasattr(self.vae, "enable_tiling"):
             self.vae.enable_tiling()
+
+    def enable_cfg_parallel(self, group=None):
+        """Single-image latency mode (no reference counterpart): the uncond and cond
+        branches run on the two ranks of `group` (torch.distributed, RCCL), exchanging their outputs once per
+        step. Every rank calls the pipeline with the same inputs and gets the same images."""
+        import torch.distributed as dist
+
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) != 2:
+            raise ValueError("enable_cfg_parallel needs an initialised process group of exactly 2 ranks")
+        self._cfg_group = group
+        self._cfg_parallel = True
+
+    def disable_cfg_parallel(self):
+        self._cfg_parallel = False
 
     def enable_model_cpu_offload(self, *a, **k):
         """generate.py:72 (no-op: weights stay resident in the 288 GB HBM)."""
@@ -188,15 +204,23 @@ class FLitePipeline:
         L = prompt_embeds.shape[1]
         if negative_prompt_embeds.shape[1] != L:
             raise ValueError("prompt and negative prompt embeddings must have the same length")
-        if do_cfg:
-            ctx = torch.cat([negative_prompt_embeds, prompt_embeds])  # uncond first (pipeline.py:266)
+        if self._cfg_parallel and do_cfg:
+            if apg_config.enabled:
+                raise NotImplementedError("APG is not available in the CFG-parallel mode")
+            from .distributed import cfg_parallel_sample
+
+            acc = cfg_parallel_sample(dit, latents, prompt_embeds, negative_prompt_embeds, num_inference_steps,
+                                      guidance_scale, alpha, group=self._cfg_group)
         else:
-            ctx = prompt_embeds
-        nseq = ctx.shape[0]
-        eng.prepare(nseq, lh, lw, nseq * L, num_inference_steps)
-        eng.set_context(ctx.reshape(nseq * L, -1).contiguous(), [i * L for i in range(nseq + 1)])
-        eng.sample(acc, batch_size, t_list, dt_list, guidance_scale, do_cfg, apg_config.enabled,
-                   apg_config.orthogonal_threshold, use_graph)
+            if do_cfg:
+                ctx = torch.cat([negative_prompt_embeds, prompt_embeds])  # uncond first (pipeline.py:266)
+            else:
+                ctx = prompt_embeds
+            nseq = ctx.shape[0]
+            eng.prepare(nseq, lh, lw, nseq * L, num_inference_steps)
+            eng.set_context(ctx.reshape(nseq * L, -1).contiguous(), [i * L for i in range(nseq + 1)])
+            eng.sample(acc, batch_size, t_list, dt_list, guidance_scale, do_cfg, apg_config.enabled,
+                       apg_config.orthogonal_threshold, use_graph)
 
         if output_type == "latent":
             return FLitePipelineOutput(images=acc.to(dtype))

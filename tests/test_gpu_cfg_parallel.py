@@ -56,8 +56,14 @@ def _worker(rank, port, q):
         m = DiT.random(seed=0, device="cuda", **PRESETS["tiny"])
         acc = cfg_parallel_sample(m, lat.cuda(), pos.cuda(), neg.cuda(), num_inference_steps=STEPS,
                                   guidance_scale=G)
+        pipe = FLitePipeline(m)
+        pipe.enable_cfg_parallel()
+        via_pipe = pipe(prompt_embeds=pos.cuda(), negative_prompt_embeds=neg.cuda(), latents=lat.cuda(),
+                        height=128, width=128, num_inference_steps=STEPS, guidance_scale=G,
+                        output_type="latent").images
         torch.cuda.synchronize()
         q.put((rank, acc.cpu()))
+        q.put((rank + 2, via_pipe.cpu()))
         dist.destroy_process_group()
     except Exception as e:  # report instead of leaving the parent waiting
         q.put((rank, repr(e)))
@@ -71,10 +77,16 @@ def two_rank_result():
     procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=100) for _ in range(2))
+    res = {}
+    while len(res) < 4 and not any(isinstance(v, str) for v in res.values()):
+        k, v = q.get(timeout=100)
+        res[k] = v
     for p in procs:
         p.join(30)
-    for r in (0, 1):
+        if p.is_alive():  # a rank stuck in the exchange after its peer failed
+            p.kill()
+            p.join(10)
+    for r in sorted(res):
         assert isinstance(res[r], torch.Tensor), f"rank {r}: {res[r]}"
     return res
 
@@ -106,6 +118,12 @@ def _one_process_branches():
 def test_ranks_agree_and_match_one_process(two_rank_result):
     assert torch.equal(two_rank_result[0], two_rank_result[1])
     assert torch.equal(two_rank_result[0], _one_process_branches())
+
+
+def test_pipeline_surface(two_rank_result):
+    """FLitePipeline.enable_cfg_parallel(): the same latents through the reference's __call__ surface."""
+    assert torch.equal(two_rank_result[2], two_rank_result[0].bfloat16())
+    assert torch.equal(two_rank_result[3], two_rank_result[2])
 
 
 def test_matches_batched_cfg_loop_and_oracle(two_rank_result):
