@@ -56,12 +56,55 @@ def vae_flops(H: int, W: int):
     return decoder_flops(H, W)
 
 
-def cpu_baseline_sample(model, cfg: dict, H: int, W: int, steps: int):
-    """Time the fp32 CPU oracle (oracle/flite_ref.py) on one DiT block at the full 1024^2 CFG batch and
-    extrapolate to a whole image (depth x steps); the VAE decode is not included in the CPU sample."""
-    from oracle import flite_ref as R
+def host_info():
+    """nproc, the cores this process may use, the lscpu model name and the NUMA node count."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cores"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity_cores"] = os.cpu_count()
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                info["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        info["numa_nodes"] = len([p for p in Path("/sys/devices/system/node").glob("node[0-9]*")])
+    except OSError:
+        pass
+    return info
 
-    threads = torch.get_num_threads()
+
+def cpu_threads() -> int:
+    """torch threads for the CPU baseline: every core this process may run on (sched affinity), capped by
+    OMP_NUM_THREADS when the host sets it (the GPU box grants each job a 16-core share of a larger machine)."""
+    n = host_info()["affinity_cores"]
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blocks: int = 3):
+    """The fp32 CPU port of the path (oracle/flite_ref.py + oracle/vae_ref.py, checked against the stub-loaded
+    reference's golden fixtures) timed on this node's host cores, on the same bf16 weights copied to the host.
+
+    A full CPU image is ~1.5 h at 10B 1024^2, so the sample measures every DIFFERENT piece of one image once and
+    extrapolates: (a) the per-call DiT work outside the blocks (context_proj + norm, patch embed, time embed /
+    adaLN, final stage; RefDiT at depth 0) at the CFG batch of 2, (b) `n_blocks` DiT blocks at full size (every
+    block of a layout has the same shapes), (c) one full VAE decode to uint8 when a VAE is present. Per image =
+    steps x (a + depth x b / n_blocks) + c, labelled as extrapolated. (BASELINE.md §4 plans 2 whole CFG steps
+    + VAE x15; on a 16-core share that is ~6 min of CPU, beyond the bounded sample the bench contract allows.)"""
+    import dataclasses
+
+    from oracle import flite_ref as R
+    from oracle import vae_ref as VR
+
+    threads = cpu_threads()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     D = cfg["hidden_size"]
     nh = cfg["num_heads"]
     p = cfg["patch_size"]
@@ -71,31 +114,73 @@ def cpu_baseline_sample(model, cfg: dict, H: int, W: int, steps: int):
     rcfg = R.DiTConfig(**{k: cfg[k] for k in ("in_channels", "patch_size", "hidden_size", "depth", "num_heads",
                                                  "mlp_ratio", "cross_attn_input_size", "train_bias_and_rms",
                                                  "per_block_adaln")})
-    # block 0 weights: the same bf16 tensors the GPU uses, copied to the host in fp32
-    params = {n: t.detach().float().cpu() for n, t in model.named_parameters() if n.startswith("blocks.0.")}
-    ref = R.RefDiT(rcfg, params, dtype=torch.float32)
+    n_blocks = min(n_blocks, cfg["depth"])
+    params = {n: t.detach().float().cpu() for n, t in model.named_parameters()
+              if not n.startswith("blocks.") or int(n.split(".")[1]) < n_blocks}
     g = torch.Generator().manual_seed(0)
-    x = torch.randn(B * T, D, generator=g)
-    ctx = torch.randn(B * 512, D, generator=g)
-    cu = torch.tensor([0, T, 2 * T], dtype=torch.int32)
-    ccu = torch.tensor([0, 512, 1024], dtype=torch.int32)
-    mod = tuple(0.02 * torch.randn(B * T, D, generator=g) for _ in range(9))
-    cos, sin = R.rope_tables(hp, wp, D // (2 * nh), 10000.0, 16, torch.bfloat16)
-    cos, sin = cos[None].repeat(1, B, 1), sin[None].repeat(1, B, 1)
+    res = {}
     with torch.no_grad():
+        # (a) everything outside the blocks, one CFG-batched call
+        top = R.RefDiT(dataclasses.replace(rcfg, depth=0), params, dtype=torch.float32)
+        x_lat = torch.randn(B, cfg["in_channels"], H // 8, W // 8, generator=g)
+        ctx_in = torch.randn(B, 512, cfg["cross_attn_input_size"], generator=g)
+        t_in = torch.tensor([0.75, 0.75], dtype=torch.bfloat16)
         t0 = time.perf_counter()
-        ref.block(0, x, cu, T, ctx, ccu, mod, cos, sin)
-        dt = time.perf_counter() - t0
-    per_image = dt * cfg["depth"] * steps
+        top(x_lat, ctx_in, None, t_in)
+        res["top_s"] = time.perf_counter() - t0
+        # (b) n_blocks full-size blocks
+        ref = R.RefDiT(rcfg, params, dtype=torch.float32)
+        x = torch.randn(B * T, D, generator=g)
+        ctx = torch.randn(B * 512, D, generator=g)
+        cu = torch.tensor([0, T, 2 * T], dtype=torch.int32)
+        ccu = torch.tensor([0, 512, 1024], dtype=torch.int32)
+        mod = tuple(0.02 * torch.randn(B * T, D, generator=g) for _ in range(9))
+        cos, sin = R.rope_tables(hp, wp, D // (2 * nh), 10000.0, 16, torch.bfloat16)
+        cos, sin = cos[None].repeat(1, B, 1), sin[None].repeat(1, B, 1)
+        t0 = time.perf_counter()
+        for i in range(n_blocks):
+            x = ref.block(i, x, cu, T, ctx, ccu, mod, cos, sin)
+        res["block_s"] = (time.perf_counter() - t0) / n_blocks
+        # (c) one VAE decode to uint8
+        res["vae_s"] = 0.0
+        if vae is not None:
+            vparams = {n: t.detach().float().cpu() for n, t in vae.named_parameters()}
+            dec = VR.RefVAEDecoder(vparams)
+            z = torch.randn(1, 16, H // 8, W // 8, generator=g)
+            t0 = time.perf_counter()
+            VR.decode_to_uint8(dec, z)
+            res["vae_s"] = time.perf_counter() - t0
+    torch.set_num_threads(prev_threads)
+    per_image = steps * (res["top_s"] + cfg["depth"] * res["block_s"]) + res["vae_s"]
     return {
         "value": 1.0 / per_image,
         "unit": "images/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"fp32 CPU oracle (oracle/flite_ref.py), 1 of {cfg['depth']} DiT blocks x 1 of {steps} steps "
-                   f"at {H}x{W} CFG batch 2 (T={T}) measured {dt:.2f} s, extrapolated x{cfg['depth'] * steps} "
-                   "per image; VAE decode excluded"),
+        "extrapolated": True,
+        "sample": (f"fp32 CPU port (oracle/flite_ref.py, oracle/vae_ref.py) at {H}x{W}, CFG batch 2 (T={T}): "
+                   f"per-call non-block DiT work {res['top_s']:.2f} s, {n_blocks} of {cfg['depth']} blocks "
+                   f"{res['block_s']:.2f} s each, VAE decode {res['vae_s']:.2f} s; per image = {steps} x "
+                   f"({res['top_s']:.2f} + {cfg['depth']} x {res['block_s']:.2f}) + {res['vae_s']:.2f} = "
+                   f"{per_image:.0f} s (EXTRAPOLATED from the measured components)"),
+        "host": host_info(),
+        "components_s": {k: round(v, 3) for k, v in res.items()},
     }
+
+
+def relaunch_distributed(n: int) -> int:
+    """`bench.py --gpus N` run without torchrun: start the N ranks as a child torch.distributed.run (one process
+    per GPU, 127.0.0.1 rendezvous) and return its exit code. Called before anything touches the GPU."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -116,9 +201,16 @@ def main():
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun around us: launch the N ranks ourselves (nothing has touched the GPU yet)
+        raise SystemExit(relaunch_distributed(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
@@ -126,6 +218,8 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     from f_lite import DiT, FLitePipeline
     from f_lite import _native as nat
@@ -238,8 +332,8 @@ def main():
             except Exception:
                 pass
     cpu = None
-    if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline_sample(model, cfg, args.height, args.width, args.sample_steps)
+    if not args.no_cpu_baseline:  # rank 0 only (the other ranks have returned), at every N
+        cpu = cpu_baseline_sample(model, vae, cfg, args.height, args.width, args.sample_steps)
 
     metric = "images/sec @%dx%d, %d steps, F-Lite-%s bf16" % (args.width, args.height, args.sample_steps,
                                                               args.model.upper())
@@ -265,6 +359,9 @@ def main():
             "VAE decode to uint8" if vae is not None else "latents only (no VAE)"),
                    "images_per_gpu_per_step": 1, "cfg_batch": 2, "parallelism": "replica dp%d" % world,
                    "hipgraph": not args.no_graph, "vae_tiling": bool(args.vae_tiling)},
+        "distributed": {"world_size": world, "backend": "nccl (RCCL over xGMI)" if world > 1 else "none",
+                        "collectives": "one broadcast of the [1,512,4096] context from rank 0 before the loop",
+                        "images_per_rank": args.steps},
         "mfma_util_image": round(f_image * value / world / PEAK_BF16, 4),
         "algorithmic_flops_per_image": f_image,
         "roofline": roofline,

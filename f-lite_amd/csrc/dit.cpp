@@ -81,6 +81,10 @@ int DitEngine::alloc(void** p, size_t bytes) {
 int DitEngine::bind(const std::string& name, const void* ptr, long numel) {
   FLITE_REQUIRE(ptr != nullptr, "bind: null pointer for " + name);
   FLITE_REQUIRE(((uintptr_t)ptr & 15) == 0, "bind: parameter " + name + " is not 16-B aligned");
+  // a captured graph bakes every weight pointer into its kernel arguments: rebinding to new storage
+  // invalidates it (the next sample() recaptures)
+  auto old = bound_.find(name);
+  if (old == bound_.end() || old->second.first != ptr) drop_graph();
   bound_[name] = {ptr, numel};
   const bf16_t* p = (const bf16_t*)ptr;
   const long DD = (long)D * D;

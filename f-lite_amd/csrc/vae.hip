@@ -278,7 +278,9 @@ int grid_of(long total) {
 
 int group_norm(const bf16_t* x, bf16_t* y, long rows, int C, int G, const bf16_t* gamma, const bf16_t* beta,
                float eps, bool silu, double* stats, hipStream_t s) {
-  FLITE_REQUIRE(C % G == 0 && C % 8 == 0 && C / G >= 4 && (C / G) % 4 == 0, "group_norm: unsupported channels");
+  // gn_stats_kernel reduces 8-channel vectors: a vector must lie inside one group (C/G a multiple of 8) or
+  // hold exactly two whole groups (C/G == 4); C/G = 12, 20, ... would straddle groups
+  FLITE_REQUIRE(C % G == 0 && C % 8 == 0 && (C / G == 4 || (C / G) % 8 == 0), "group_norm: unsupported channels");
   FLITE_REQUIRE(G <= 64, "group_norm: at most 64 groups");
   const long vecs = rows * (C / 8);
   // the grid stride (blocks * 256) must be a multiple of C/8 so that each thread stays on one channel vector

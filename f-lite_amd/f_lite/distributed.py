@@ -33,8 +33,28 @@ def broadcast_context(ctx: torch.Tensor, src: int = 0, group=None) -> torch.Tens
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.broadcast(ctx, src=src, group=group)
+        if dist.get_backend(group) == "gloo" and ctx.device.type != "cpu":  # CPU tests / ranks sharing a GPU
+            host = ctx.detach().cpu()
+            dist.broadcast(host, src=src, group=group)
+            ctx.copy_(host)
+        else:
+            dist.broadcast(ctx, src=src, group=group)
     return ctx
+
+
+def broadcast_from_group_root(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place broadcast of `t` from rank 0 OF `group` (its global rank resolved) to the group's ranks. With
+    gloo (CPU tests, or two ranks sharing one GPU) a device tensor is staged through the host."""
+    import torch.distributed as dist
+
+    src = 0 if group is None else dist.get_global_rank(group, 0)
+    if dist.get_backend(group) == "gloo" and t.device.type != "cpu":
+        host = t.detach().cpu()
+        dist.broadcast(host, src=src, group=group)
+        t.copy_(host)
+    else:
+        dist.broadcast(t, src=src, group=group)
+    return t
 
 
 def exchange_branches(out: torch.Tensor, group=None) -> "List[torch.Tensor]":
@@ -88,7 +108,15 @@ def cfg_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Tensor,
         negative_prompt_embeds.to(device=dev, dtype=torch.bfloat16)  # pipeline.py:160-161
     if neg.shape != pos.shape or pos.shape[0] != n_img:
         raise ValueError("prompt / negative embeddings must both be [n_img, L, C_ctx]")
-    ctx = (neg if rank == 0 else pos).contiguous()
+    # Both branches must integrate the SAME noise and embeddings: ranks that drew their own latents (e.g.
+    # seeded with seed + rank, or after uneven RNG use) would otherwise each return a wrong image silently.
+    # One broadcast from the group's first rank before the loop, like broadcast_context.
+    lat = latents.to(device=dev, dtype=torch.bfloat16).contiguous()
+    pos = pos.contiguous()
+    neg = neg.contiguous()
+    for t in (lat, pos, neg):
+        broadcast_from_group_root(t, group)
+    ctx = neg if rank == 0 else pos
     L = ctx.shape[1]
     sched = flow_schedule(num_inference_steps, lh, lw, alpha)
     t_list = [t for t, _ in sched]
@@ -97,7 +125,7 @@ def cfg_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Tensor,
     eng.set_context(ctx.reshape(n_img * L, -1), [i * L for i in range(n_img + 1)])
     # one timestep row per step, shared by the batch (pipeline.py:260,268), as in flite_dit_sample
     eng.set_timesteps(torch.tensor(t_list, dtype=torch.float32, device=dev), bool(eng.cfg.bf16_timestep_quant))
-    acc = latents.to(device=dev, dtype=torch.bfloat16).float().contiguous()
+    acc = lat.float().contiguous()
     out = torch.empty_like(acc)
 
     def forward_branch(x, i):

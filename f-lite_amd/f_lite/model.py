@@ -199,11 +199,16 @@ class DiT(nn.Module):
 
     # ------------------------------------------------------------------ diffusers-folder IO
     def config_dict(self):
+        """config.json as register_to_config writes it (model.py:418-433): the constructor kwargs only. The
+        layout (model.py vs model_v2.py) is not a config key: model_index.json's module names it."""
         d = {k: getattr(self.config, k) for k in _CONFIG_KEYS}
         d["_class_name"] = "DiT"
-        if self.per_block_adaln:
-            d["per_block_adaln"] = True
         return d
+
+    @property
+    def module_name(self) -> str:
+        """The reference module of this layout, as model_index.json records it (generate.py:65)."""
+        return "f_lite.model_v2" if self.per_block_adaln else "f_lite.model"
 
     def save_pretrained(self, save_directory):
         from safetensors.torch import save_file
@@ -227,15 +232,25 @@ class DiT(nn.Module):
         if not (p / "config.json").exists():
             raise FileNotFoundError(f"{p}/config.json not found (only local diffusers-layout folders are supported)")
         cfg = json.loads((p / "config.json").read_text())
-        cfg = {k: v for k, v in cfg.items() if not k.startswith("_")}
-        m = cls.empty(device=device, dtype=torch_dtype, **cfg)
+        cfg = {k: v for k, v in cfg.items() if not k.startswith("_") and k in _CONFIG_KEYS + ("per_block_adaln",)}
         files = sorted(p.glob("diffusion_pytorch_model*.safetensors"))
         if not files:
             raise FileNotFoundError(f"no diffusion_pytorch_model*.safetensors in {p}")
         sd = {}
         for f in files:
             sd.update(load_file(str(f)))
-        sd = {k.replace("module.", "").replace("_orig_mod.", ""): v for k, v in sd.items()}  # pt.py:98-101
+        return cls.from_state_dict(clean_state_dict(sd), device=device, torch_dtype=torch_dtype, **cfg)
+
+    @classmethod
+    def from_state_dict(cls, sd, device="cuda", torch_dtype=torch.bfloat16, **cfg):
+        """Build on `device` in `torch_dtype` and load `sd` strictly. A per-block-adaLN state dict given to the
+        model.py class (or the reverse) is refused with the class to use instead."""
+        m = cls.empty(device=device, dtype=torch_dtype, **cfg)
+        v2_keys = any(k.startswith("blocks.") and ".adaLN_modulation." in k for k in sd)
+        if v2_keys != m.per_block_adaln:
+            want = "f_lite.model_v2.DiT" if v2_keys else "f_lite.model.DiT"
+            raise ValueError(f"state dict is the {'model_v2' if v2_keys else 'model'}.py layout: load it with {want} "
+                             "(model_index.json dit_model module)")
         m.load_state_dict(sd, strict=True)
         return m
 
@@ -334,6 +349,11 @@ class DiT(nn.Module):
             xin = xin.float()
         eng.forward(xin, out, 0, 1)
         return out
+
+
+def clean_state_dict(sd):
+    """Strip the DDP / torch.compile key prefixes, as load_f_lite_pt does (pt.py:98-101)."""
+    return {k.replace("module.", "").replace("_orig_mod.", ""): v for k, v in sd.items()}
 
 
 def _is_norm_weight(name: str) -> bool:

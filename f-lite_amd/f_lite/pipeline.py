@@ -44,6 +44,17 @@ class FLitePipelineOutput:
     images: Union[List["Image.Image"], np.ndarray, torch.Tensor]  # noqa: F821
 
 
+def randn_tensor(shape, generator=None, device=None, dtype=None):
+    """diffusers.utils.torch_utils.randn_tensor semantics (pipeline.py:236): draw on the generator's device
+    (a CPU generator gives the same noise whatever the target device), then move to `device`."""
+    if isinstance(generator, (list, tuple)):  # one generator per image, as diffusers allows
+        if len(generator) != shape[0]:
+            raise ValueError(f"{len(generator)} generators for a batch of {shape[0]}")
+        return torch.cat([randn_tensor((1,) + tuple(shape[1:]), g, device, dtype) for g in generator])
+    gen_dev = generator.device if generator is not None else torch.device(device or "cpu")
+    return torch.randn(shape, generator=generator, device=gen_dev, dtype=dtype).to(device)
+
+
 def flow_schedule(num_inference_steps: int, latent_h: int, latent_w: int, alpha: Optional[float] = None):
     """Shifted rectified-flow schedule (pipeline.py:239-257): [(t, dt)], t in python float64."""
     if alpha is None:
@@ -56,6 +67,22 @@ def flow_schedule(num_inference_steps: int, latent_h: int, latent_w: int, alpha:
         tn = tn * alpha / (1 + (alpha - 1) * tn)
         out.append((t, t - tn))
     return out
+
+
+def resolve_dit_class(entry):
+    """model_index.json's ["module", "class"] for dit_model -> the DiT class. The reference registers the DiT
+    with diffusers' loader under "f_lite" and "f_lite.model" (generate.py:61-66); a model_v2.py folder names
+    "f_lite.model_v2" (per-block adaLN, the 10B layout)."""
+    module, cls = entry
+    if cls != "DiT":
+        raise ValueError(f"dit_model: unsupported class {module}.{cls}")
+    if module in ("f_lite", "f_lite.model"):
+        return DiT
+    if module == "f_lite.model_v2":
+        from .model_v2 import DiT as DiTv2
+
+        return DiTv2
+    raise ValueError(f"dit_model: unknown module {module!r} (expected f_lite.model or f_lite.model_v2)")
 
 
 class FLitePipeline:
@@ -82,9 +109,8 @@ class FLitePipeline:
         if not (root / "model_index.json").exists():
             raise FileNotFoundError(f"{root}/model_index.json not found (Hub names cannot be resolved offline)")
         index = json.loads((root / "model_index.json").read_text())
-        dit = DiT.from_pretrained(root, subfolder="dit_model", torch_dtype=torch_dtype, device=device)
-        if "per_block_adaln" in json.loads((root / "dit_model" / "config.json").read_text()):
-            dit.per_block_adaln = True
+        dit_cls = resolve_dit_class(index.get("dit_model", ["f_lite.model", "DiT"]))
+        dit = dit_cls.from_pretrained(root, subfolder="dit_model", torch_dtype=torch_dtype, device=device)
         vae = None
         if "vae" in index and (root / "vae").exists():
             from .vae import AutoencoderKL
@@ -95,7 +121,7 @@ class FLitePipeline:
     def save_pretrained(self, path):
         root = Path(path)
         root.mkdir(parents=True, exist_ok=True)
-        index = {"_class_name": "FLitePipeline", "dit_model": ["f_lite.model", "DiT"]}
+        index = {"_class_name": "FLitePipeline", "dit_model": [self.dit_model.module_name, "DiT"]}
         self.dit_model.save_pretrained(root / "dit_model")
         if self.vae is not None:
             index["vae"] = ["diffusers", "AutoencoderKL"]
@@ -189,7 +215,7 @@ class FLitePipeline:
         # 3. initial latents (pipeline.py:228-237): randn in the model dtype, same generator semantics
         lh, lw = height // self.vae_scale_factor, width // self.vae_scale_factor
         if latents is None:
-            latents = torch.randn((batch_size, 16, lh, lw), generator=generator, device=device, dtype=dtype)
+            latents = randn_tensor((batch_size, 16, lh, lw), generator=generator, device=device, dtype=dtype)
         latents = latents.to(device=device, dtype=dtype)
         acc = latents.float().contiguous()  # fp32 Euler accumulator (reference: model dtype)
 

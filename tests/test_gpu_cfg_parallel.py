@@ -61,9 +61,18 @@ def _worker(rank, port, q):
         via_pipe = pipe(prompt_embeds=pos.cuda(), negative_prompt_embeds=neg.cuda(), latents=lat.cuda(),
                         height=128, width=128, num_inference_steps=STEPS, guidance_scale=G,
                         output_type="latent").images
+        # latents=None with a DIFFERENT seed per rank: the ranks must still integrate rank 0's noise
+        own = pipe(prompt_embeds=pos.cuda(), negative_prompt_embeds=neg.cuda(), height=128, width=128,
+                   num_inference_steps=STEPS, guidance_scale=G, output_type="latent",
+                   generator=torch.Generator().manual_seed(100 + rank)).images
+        lat0 = torch.randn(1, 16, 16, 16, generator=torch.Generator().manual_seed(100), dtype=torch.bfloat16)
+        explicit = cfg_parallel_sample(m, lat0.cuda(), pos.cuda(), neg.cuda(), num_inference_steps=STEPS,
+                                       guidance_scale=G)
         torch.cuda.synchronize()
         q.put((rank, acc.cpu()))
         q.put((rank + 2, via_pipe.cpu()))
+        q.put((rank + 4, own.cpu()))
+        q.put((rank + 6, explicit.cpu()))
         dist.destroy_process_group()
     except Exception as e:  # report instead of leaving the parent waiting
         q.put((rank, repr(e)))
@@ -78,7 +87,7 @@ def two_rank_result():
     for p in procs:
         p.start()
     res = {}
-    while len(res) < 4 and not any(isinstance(v, str) for v in res.values()):
+    while len(res) < 8 and not any(isinstance(v, str) for v in res.values()):
         k, v = q.get(timeout=100)
         res[k] = v
     for p in procs:
@@ -124,6 +133,14 @@ def test_pipeline_surface(two_rank_result):
     """FLitePipeline.enable_cfg_parallel(): the same latents through the reference's __call__ surface."""
     assert torch.equal(two_rank_result[2], two_rank_result[0].bfloat16())
     assert torch.equal(two_rank_result[3], two_rank_result[2])
+
+
+def test_per_rank_seeds_are_unified(two_rank_result):
+    """Ranks seeded differently (latents=None, generator seed 100 + rank) integrate rank 0's noise and end
+    equal to each other and to an explicit run on rank 0's latents (broadcast before the loop)."""
+    assert torch.equal(two_rank_result[4], two_rank_result[5])
+    assert torch.equal(two_rank_result[4], two_rank_result[6].bfloat16())
+    assert torch.equal(two_rank_result[6], two_rank_result[7])
 
 
 def test_matches_batched_cfg_loop_and_oracle(two_rank_result):

@@ -1,0 +1,152 @@
+"""CPU: the loading surface of the drop-in -- diffusers-folder round trips for both layouts (model_index.json's
+dit_model module decides, generate.py:61-68), raw .pt checkpoints (pt.py:78-104), and the f_lite.generate CLI
+(generate.py:13-116: arguments, defaults, output naming). No kernels run here."""
+import inspect
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+from f_lite import DiT, FLitePipeline
+from f_lite.model import PRESETS
+from f_lite.model_v2 import DiT as DiTv2
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _filled(cls, preset, seed=0):
+    cfg = dict(PRESETS[preset])
+    m = cls(**cfg)
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn(p.shape, generator=g))
+    return m
+
+
+def _same_weights(a, b):
+    sa, sb = a.state_dict(), b.state_dict()
+    return set(sa) == set(sb) and all(torch.equal(sa[k].float(), sb[k].float()) for k in sa)
+
+
+@pytest.mark.parametrize("preset,module", [("tiny", "f_lite.model"), ("tiny_v2", "f_lite.model_v2")])
+def test_pipeline_folder_round_trip(tmp_path, preset, module):
+    m = _filled(DiT, preset)
+    FLitePipeline(m).save_pretrained(tmp_path)
+    index = json.loads((tmp_path / "model_index.json").read_text())
+    assert index["dit_model"] == [module, "DiT"]
+    cfg = json.loads((tmp_path / "dit_model" / "config.json").read_text())
+    assert "per_block_adaln" not in cfg  # reference config.json keys only (model.py:419-433)
+    pipe = FLitePipeline.from_pretrained(tmp_path, torch_dtype=torch.float32, device="cpu")
+    assert isinstance(pipe.dit_model, DiTv2 if module.endswith("v2") else DiT)
+    assert pipe.dit_model.per_block_adaln == module.endswith("v2")
+    assert _same_weights(pipe.dit_model, m)
+
+
+def test_reference_shaped_v2_folder(tmp_path):
+    """A folder as the reference would save a model_v2 DiT: ["f_lite.model_v2", "DiT"] and no layout key."""
+    m = _filled(DiTv2, "tiny_v2")
+    (tmp_path / "dit_model").mkdir(parents=True)
+    m.save_pretrained(tmp_path / "dit_model")
+    (tmp_path / "model_index.json").write_text(json.dumps(
+        {"_class_name": "FLitePipeline", "dit_model": ["f_lite.model_v2", "DiT"],
+         "vae": ["diffusers", "AutoencoderKL"], "text_encoder": ["transformers", "T5EncoderModel"]}))
+    pipe = FLitePipeline.from_pretrained(tmp_path, torch_dtype=torch.float32, device="cpu")
+    assert pipe.dit_model.per_block_adaln and _same_weights(pipe.dit_model, m)
+
+
+def test_layout_mismatch_is_refused(tmp_path):
+    m = _filled(DiTv2, "tiny_v2")
+    FLitePipeline(m).save_pretrained(tmp_path)
+    idx = json.loads((tmp_path / "model_index.json").read_text())
+    idx["dit_model"] = ["f_lite.model", "DiT"]  # wrong module for per-block adaLN weights
+    (tmp_path / "model_index.json").write_text(json.dumps(idx))
+    with pytest.raises(ValueError, match="model_v2"):
+        FLitePipeline.from_pretrained(tmp_path, torch_dtype=torch.float32, device="cpu")
+    idx["dit_model"] = ["somewhere.else", "DiT"]
+    (tmp_path / "model_index.json").write_text(json.dumps(idx))
+    with pytest.raises(ValueError, match="unknown module"):
+        FLitePipeline.from_pretrained(tmp_path, torch_dtype=torch.float32, device="cpu")
+
+
+@pytest.mark.parametrize("preset", ["tiny", "tiny_v2"])
+def test_pt_checkpoint(tmp_path, preset):
+    """load_f_lite_pt: depth from the block indices, heads = width // 256, DDP / compile prefixes stripped."""
+    from f_lite.pt import infer_dit_config, load_f_lite_pt
+
+    m = _filled(DiT, preset)
+    sd = {("module._orig_mod." if i % 2 else "") + k: v for i, (k, v) in enumerate(m.state_dict().items())}
+    path = tmp_path / "ckpt.pt"
+    torch.save(sd, path)
+    cfg = infer_dit_config({k.replace("module.", "").replace("_orig_mod.", ""): v for k, v in sd.items()},
+                           width=512, cross_attn_input_size=128, train_bias_and_rms=True)
+    assert cfg["depth"] == PRESETS[preset]["depth"] and cfg["num_heads"] == 2
+    assert cfg["per_block_adaln"] == PRESETS[preset]["per_block_adaln"]
+    pipe = load_f_lite_pt(path, "cpu", dtype="bfloat16", width=512, cross_attn_input_size=128,
+                          train_bias_and_rms=True)
+    assert pipe.dit_model.dtype == torch.bfloat16
+    ref = {k: v.bfloat16() for k, v in m.state_dict().items()}
+    got = pipe.dit_model.state_dict()
+    assert set(got) == set(ref) and all(torch.equal(got[k], ref[k]) for k in ref)
+
+
+def test_pt_checkpoint_errors(tmp_path):
+    from f_lite.pt import load_f_lite_pt
+
+    m = _filled(DiT, "tiny")
+    sd = m.state_dict()
+    sd.pop("final_proj.bias")
+    torch.save(sd, tmp_path / "bad.pt")
+    with pytest.raises(KeyError):
+        load_f_lite_pt(tmp_path / "bad.pt", "cpu", width=512, cross_attn_input_size=128, train_bias_and_rms=True)
+    with pytest.raises(NotImplementedError):
+        load_f_lite_pt(tmp_path / "bad.pt", "cpu", residual_v=True)
+    with pytest.raises(NotImplementedError):
+        load_f_lite_pt(tmp_path / "bad.pt", "cpu", lora_path="x")
+
+
+def test_generate_signature_matches_reference():
+    """generate_images keeps the reference's parameters and defaults (generate.py:13-25)."""
+    from f_lite.generate import build_parser, generate_images
+
+    sig = inspect.signature(generate_images)
+    ref = dict(prompt=inspect.Parameter.empty, output_file=inspect.Parameter.empty, model="Freepik/F-Lite",
+               negative_prompt=None, seed=0, guidance_scale=6, steps=30, width=1344, height=896, cpu_offload=True,
+               device=None, num_images=1)
+    for k, v in ref.items():
+        assert sig.parameters[k].default == v, k
+    args = build_parser().parse_args(["--prompt", "a cat", "--output_file", "o.png"])
+    for k, v in ref.items():
+        if v is not inspect.Parameter.empty:
+            assert getattr(args, k) == v, k
+
+
+def test_generate_output_naming():
+    from f_lite.generate import output_paths
+
+    assert output_paths("out/img.png", 1) == [Path("out/img.png")]
+    assert output_paths("out/img.png", 3) == [Path("out/img.png"), Path("out/img-1.png"), Path("out/img-2.png")]
+
+
+def test_generate_fails_loudly_without_gpu(tmp_path):
+    from f_lite._native import FliteError
+    from f_lite.generate import generate_images
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(FliteError):
+        generate_images("a cat", str(tmp_path / "x.png"), model="random:tiny")
+    with pytest.raises(FliteError):
+        generate_images("a cat", str(tmp_path / "x.png"), model="random:tiny", device="cpu")
+
+
+def test_bench_refuses_world_size_mismatch():
+    """bench.py --gpus N must run one rank per GPU: a torchrun world of another size is refused before any GPU
+    call (here WORLD_SIZE=1 with --gpus 2)."""
+    env = dict(__import__("os").environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode != 0 and "one rank per GPU" in r.stderr
