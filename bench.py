@@ -28,6 +28,7 @@ sys.path.insert(0, str(ROOT))
 import torch  # noqa: E402
 
 PEAK_BF16 = 256 * 4 * 1024 * 2.4e9  # 2.5166 PF/s dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8 = 2 * PEAK_BF16  # dense fp8 (block-scaled MFMA: 2x the bf16 rate per clock, MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
 
 
@@ -198,6 +199,8 @@ def main():
     ap.add_argument("--vae-tiling", action="store_true",
                     help="pipe.enable_vae_tiling() as generate.py:77-78 does (tiled decode above 1024 px)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fp8", action="store_true",
+                    help="BASELINE configs[4]: block GEMMs on MXFP8 weights + activations (block-scaled fp8 MFMA)")
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
     args = ap.parse_args()
 
@@ -228,6 +231,8 @@ def main():
 
     cfg = dict(PRESETS[args.model])
     model = DiT.random(seed=0, device=dev, **cfg)
+    if args.fp8:
+        model.enable_fp8(True)
     vae = None
     if not args.no_vae:
         from f_lite.vae import AutoencoderKL
@@ -312,12 +317,14 @@ def main():
         avg_ms = sum(probe_ms) / len(probe_ms)
         flops, what = per_launch[args.probe]
         achieved = flops / (avg_ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(PEAK_BF16 / 1e12, 1),
-                    "unit": "TFLOP/s", "frac": round(achieved * 1e12 / PEAK_BF16, 4), "traffic": None,
+        fp8_kernel = args.fp8 and args.probe in ("gateup", "down", "qkv")
+        peak = PEAK_FP8 if fp8_kernel else PEAK_BF16
+        roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak / 1e12, 1),
+                    "unit": "TFLOP/s", "frac": round(achieved * 1e12 / peak, 4), "traffic": None,
                     "kernel": what, "launches": len(probe_ms), "avg_ms": round(avg_ms, 4),
                     "algorithmic_flops_per_launch": flops}
         pmc = ROOT / "profiles" / "pmc_traffic.json"
-        if pmc.exists():
+        if pmc.exists() and not args.fp8:
             try:
                 tr = json.loads(pmc.read_text()).get(args.probe)
                 if tr:
@@ -335,9 +342,9 @@ def main():
     if not args.no_cpu_baseline:  # rank 0 only (the other ranks have returned), at every N
         cpu = cpu_baseline_sample(model, vae, cfg, args.height, args.width, args.sample_steps)
 
-    metric = "images/sec @%dx%d, %d steps, F-Lite-%s bf16" % (args.width, args.height, args.sample_steps,
-                                                              args.model.upper())
-    if (args.model, args.height, args.width, args.sample_steps) == ("10b", 1024, 1024, 30):
+    metric = "images/sec @%dx%d, %d steps, F-Lite-%s %s" % (args.width, args.height, args.sample_steps,
+                                                            args.model.upper(), "fp8" if args.fp8 else "bf16")
+    if (args.model, args.height, args.width, args.sample_steps, args.fp8) == ("10b", 1024, 1024, 30, False):
         metric += "; 1/8 GPU + MFMA util%"  # BASELINE.json's metric string (util in mfma_util_image)
     line = {
         "metric": metric,
@@ -350,7 +357,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": ("fp8 (MXFP8: OCP e4m3 weights+activations, E8M0 scale per 32; block GEMMs) + bf16 attention"
+                  if args.fp8 else "bf16"),
         "data": "synthetic (random-init weights from the deterministic generator; synthetic T5 context "
                 "[1,512,4096]; seeded latents)",
         "config": {"workload": "F-Lite-%s %s, %dx%d, %d steps, CFG %.1f, %s" % (
@@ -363,6 +371,7 @@ def main():
                         "collectives": "one broadcast of the [1,512,4096] context from rank 0 before the loop",
                         "images_per_rank": args.steps},
         "mfma_util_image": round(f_image * value / world / PEAK_BF16, 4),
+        "mfma_util_image_peak": "bf16 dense (2.5166 PF) for both dtypes" if args.fp8 else "bf16 dense",
         "algorithmic_flops_per_image": f_image,
         "roofline": roofline,
         "cpu_baseline": cpu,

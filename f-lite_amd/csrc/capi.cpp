@@ -6,6 +6,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "dit.h"
+#include "fp8.h"
 #include <math.h>
 
 namespace flite {
@@ -314,5 +315,81 @@ int flite_group_norm(void* stream, const void* x, void* y, long rows, int channe
                      const void* beta, float eps, int silu, double* stats_workspace) {
   return group_norm((const bf16_t*)x, (bf16_t*)y, rows, channels, groups, (const bf16_t*)gamma,
                     (const bf16_t*)beta, eps, silu != 0, stats_workspace, (hipStream_t)stream);
+}
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------------------
+// MXFP8 (fp8.hip, gemm_fp8.hip)
+// ---------------------------------------------------------------------------------------------------------------
+extern "C" {
+int flite_quant_fp8_rows(void* stream, const void* src, long ld_src, long rows, int K, void* dst, long ld_dst,
+                         void* scales, long rows_pad) {
+  FLITE_REQUIRE(src && dst && scales, "flite_quant_fp8_rows: null argument");
+  return quant_rows_fp8((const bf16_t*)src, ld_src, rows, K, (uint8_t*)dst, ld_dst, (uint8_t*)scales, rows_pad,
+                        (hipStream_t)stream);
+}
+
+int flite_quant_fp8_gateup(void* stream, const void* gate, const void* up, long ld_src, int F, int K, void* dst,
+                           void* scales) {
+  FLITE_REQUIRE(gate && up && dst && scales, "flite_quant_fp8_gateup: null argument");
+  return quant_gateup_fp8((const bf16_t*)gate, (const bf16_t*)up, ld_src, F, K, (uint8_t*)dst, (uint8_t*)scales,
+                          (hipStream_t)stream);
+}
+
+int flite_gemm_fp8(void* stream, int M, int N, int K, const void* A8, long lda, const void* a_scales,
+                   long a_rows_pad, const void* W8, long ldw, const void* w_scales, long w_rows_pad,
+                   const void* bias, int epilogue, void* out, long ldo, void* out_scales, long out_rows_pad,
+                   const float* gate, long gate_seg_stride, int rows_per_seg) {
+  FLITE_REQUIRE(A8 && a_scales && W8 && w_scales && out, "flite_gemm_fp8: null argument");
+  GemmFp8Params p;
+  p.A = (const uint8_t*)A8;
+  p.lda = lda;
+  p.As = (const uint8_t*)a_scales;
+  p.a_rows_pad = a_rows_pad;
+  p.W = (const uint8_t*)W8;
+  p.ldw = ldw;
+  p.Ws = (const uint8_t*)w_scales;
+  p.w_rows_pad = w_rows_pad;
+  p.bias = (const bf16_t*)bias;
+  p.out = out;
+  p.ldo = ldo;
+  p.out_sc = (uint8_t*)out_scales;
+  p.out_rows_pad = out_rows_pad;
+  p.gate = gate;
+  p.gate_seg_stride = gate_seg_stride;
+  p.rows_per_seg = rows_per_seg;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  return gemm_fp8(p, epilogue, (hipStream_t)stream);
+}
+
+int flite_rmsnorm_modulate_fp8(void* stream, const float* x, long ldx, void* y8, long ldy, void* y_scales,
+                               long rows_pad, const void* w, const float* shift, const float* scale,
+                               long mod_seg_stride, long seg_rows, long rows, int dim, float eps) {
+  FLITE_REQUIRE(x && y8 && y_scales, "flite_rmsnorm_modulate_fp8: null argument");
+  NormModParams p;
+  p.x = x;
+  p.ldx = ldx;
+  p.y8 = (uint8_t*)y8;
+  p.ldy = ldy;
+  p.ysc = (uint8_t*)y_scales;
+  p.ysc_rows_pad = rows_pad;
+  p.w = (const bf16_t*)w;
+  p.shift = shift;
+  p.scale = scale;
+  p.mod_seg_stride = mod_seg_stride;
+  p.rows = rows;
+  p.D = dim;
+  p.eps = eps;
+  p.in_seg = seg_rows;
+  p.in_stride = seg_rows;
+  p.in_off = 0;
+  return rmsnorm_mod(p, false, (hipStream_t)stream);
+}
+
+int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable) {
+  FLITE_REQUIRE(dit, "flite_dit_enable_fp8: null engine");
+  return dit->eng->enable_fp8((hipStream_t)stream, enable != 0);
 }
 }  // extern "C"

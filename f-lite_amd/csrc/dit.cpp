@@ -39,6 +39,7 @@ DitEngine::DitEngine(const flite_dit_config& c) : cfg(c) {
 
 DitEngine::~DitEngine() {
   drop_graph();
+  free_fp8_weights();
   free_ws();
   if (gstream_) hipStreamDestroy(gstream_);
   if (ev_in_) hipEventDestroy(ev_in_);
@@ -61,6 +62,13 @@ void DitEngine::free_ws() {
   sk_flags_ = nullptr;
   attn_ws_ = nullptr;
   attn_ws_bytes_ = 0;
+  nbuf8_ = nbuf8_s_ = obuf8_ = obuf8_s_ = hbuf8_ = hbuf8_s_ = nullptr;
+}
+
+void DitEngine::free_fp8_weights() {
+  for (void* p : w8_allocs_) hipFree(p);
+  w8_allocs_.clear();
+  w8_.clear();
 }
 
 // every GEMM of the engine may use the stream-K workspace (launches on the engine's streams are ordered)
@@ -84,7 +92,13 @@ int DitEngine::bind(const std::string& name, const void* ptr, long numel) {
   // a captured graph bakes every weight pointer into its kernel arguments: rebinding to new storage
   // invalidates it (the next sample() recaptures)
   auto old = bound_.find(name);
-  if (old == bound_.end() || old->second.first != ptr) drop_graph();
+  if (old == bound_.end() || old->second.first != ptr) {
+    drop_graph();
+    if (!w8_.empty()) {  // the fp8 copies were quantised from the old storage
+      free_fp8_weights();
+      fp8_ = false;
+    }
+  }
   bound_[name] = {ptr, numel};
   const bf16_t* p = (const bf16_t*)ptr;
   const long DD = (long)D * D;
@@ -231,6 +245,7 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   for (int i = 0; i < 64; ++i) inv[i] = (float)(1.0 / pow((double)cfg.rope_base, (double)(2 * i) / (double)rdim));
   FLITE_HIP_CHECK(hipMemcpy(inv_freq_, inv, sizeof(inv), hipMemcpyHostToDevice));
   if (rope_table(inv_freq_, cos_, sin_, Hl / P, Wl / P, R, cfg.bf16_rope_tables, 0)) return 1;
+  if (fp8_ && alloc_fp8_act()) return 1;
   FLITE_HIP_CHECK(hipDeviceSynchronize());
   nctx_ = 0;
   nt_ = 0;
@@ -536,6 +551,183 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   return 0;
 }
 
+int DitEngine::alloc_fp8_act() {
+  if (nbuf8_ != nullptr || x_ == nullptr) return 0;
+  mpad_ = mx_rows_pad(M_);
+  const size_t sd = (size_t)(D / 128) * mpad_ * 4, sf = (size_t)(F / 128) * mpad_ * 4;
+  if (alloc((void**)&nbuf8_, (size_t)M_ * D)) return 1;
+  if (alloc((void**)&obuf8_, (size_t)M_ * D)) return 1;
+  if (alloc((void**)&hbuf8_, (size_t)M_ * F)) return 1;
+  if (alloc((void**)&nbuf8_s_, sd)) return 1;
+  if (alloc((void**)&obuf8_s_, sd)) return 1;
+  if (alloc((void**)&hbuf8_s_, sf)) return 1;
+  // pad rows of the scale arrays are staged by the GEMM (256-row tiles) but never written: zero = 2^-127
+  FLITE_HIP_CHECK(hipMemset(nbuf8_s_, 0, sd));
+  FLITE_HIP_CHECK(hipMemset(obuf8_s_, 0, sd));
+  FLITE_HIP_CHECK(hipMemset(hbuf8_s_, 0, sf));
+  return 0;
+}
+
+int DitEngine::enable_fp8(hipStream_t s, bool on) {
+  drop_graph();
+  if (!on) {
+    fp8_ = false;
+    return 0;
+  }
+  if (check_bound()) return 2;
+  FLITE_REQUIRE(D % 128 == 0 && F % 128 == 0, "fp8: hidden and MLP widths must be multiples of 128");
+  if (w8_.empty()) {
+    w8_.resize(cfg.depth);
+    auto buf = [&](uint8_t** p, size_t bytes) -> int {
+      FLITE_HIP_CHECK(hipMalloc((void**)p, bytes));
+      w8_allocs_.push_back(*p);
+      return 0;
+    };
+    // weight [rows, K] -> fp8 + scales [K/128][rows][4] (rows are multiples of 256 for every DiT weight)
+    auto q = [&](const bf16_t* w, long rows, int K, uint8_t** d, uint8_t** sc) -> int {
+      FLITE_REQUIRE(rows % 256 == 0, "fp8: weight rows must be a multiple of 256");
+      if (buf(d, (size_t)rows * K) || buf(sc, (size_t)(K / 128) * rows * 4)) return 1;
+      return quant_rows_fp8(w, K, rows, K, *d, K, *sc, rows, s);
+    };
+    for (int i = 0; i < cfg.depth; ++i) {
+      const BlockW& b = w_.blocks[i];
+      Fp8W& f = w8_[i];
+      if (q(b.qkv_w, 3L * D, D, &f.qkv, &f.qkv_s) || q(b.proj_w, D, D, &f.proj, &f.proj_s) ||
+          q(b.down_w, D, F, &f.down, &f.down_s))
+        return 1;
+      if (b.cross && (q(b.cq_w, D, D, &f.cq, &f.cq_s) || q(b.cproj_w, D, D, &f.cproj, &f.cproj_s))) return 1;
+      if (buf(&f.gu, (size_t)2 * F * D) || buf(&f.gu_s, (size_t)(D / 128) * 2 * F * 4)) return 1;
+      if (quant_gateup_fp8(b.gate_w, b.up_w, D, F, D, f.gu, f.gu_s, s)) return 1;
+    }
+    FLITE_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  fp8_ = true;
+  return alloc_fp8_act();
+}
+
+// One DiTBlock in fp8 (flite_dit_enable_fp8): the six block GEMMs on MXFP8 operands; attention, RoPE / QK-norm,
+// the residual stream and the modulation stay as in run_block.
+int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg) {
+  const BlockW& b = w_.blocks[blk];
+  const Fp8W& q = w8_[blk];
+  const float *shift_sa = mod, *scale_sa = mod + D, *gate_sa = mod + 2L * D;
+  const float *shift_ca = mod + 3L * D, *scale_ca = mod + 4L * D, *gate_ca = mod + 5L * D;
+  const float *shift_mlp = mod + 6L * D, *scale_mlp = mod + 7L * D, *gate_mlp = mod + 8L * D;
+  auto norm8 = [&](const bf16_t* w, const float* sh, const float* sc) -> int {
+    NormModParams nm;
+    nm.x = x_;
+    nm.ldx = D;
+    nm.y8 = nbuf8_;
+    nm.ldy = D;
+    nm.ysc = nbuf8_s_;
+    nm.ysc_rows_pad = mpad_;
+    nm.w = w;
+    nm.shift = sh;
+    nm.scale = sc;
+    nm.mod_seg_stride = mseg;
+    nm.rows = M_;
+    nm.D = D;
+    nm.in_seg = T_;
+    nm.in_stride = T_;
+    nm.in_off = 0;
+    return rmsnorm_mod(nm, false, s);
+  };
+  auto g8 = [&](const uint8_t* A, const uint8_t* As, const uint8_t* W, const uint8_t* Ws, long w_rows, int N, int K,
+                const bf16_t* bias, int epi, void* out, long ldo, const float* gate) -> int {
+    GemmFp8Params g;
+    g.A = A;
+    g.lda = K;
+    g.As = As;
+    g.a_rows_pad = mpad_;
+    g.W = W;
+    g.ldw = K;
+    g.Ws = Ws;
+    g.w_rows_pad = w_rows;
+    g.bias = bias;
+    g.out = out;
+    g.ldo = ldo;
+    g.gate = gate;
+    g.gate_seg_stride = mseg;
+    g.rows_per_seg = T_;
+    g.M = (int)M_;
+    g.N = N;
+    g.K = K;
+    if (epi == EPI8_SWIGLU_FP8) {
+      g.out_sc = hbuf8_s_;
+      g.out_rows_pad = mpad_;
+    }
+    return gemm_fp8(g, epi, s);
+  };
+  auto attn = [&](const bf16_t* qp, long ldq, const bf16_t* kp, const bf16_t* vp, long ldkv, const int* cu_k,
+                  int max_k) -> int {
+    AttnParams a;
+    a.q = qp;
+    a.k = kp;
+    a.v = vp;
+    a.o = obuf_;
+    a.q_row_stride = ldq;
+    a.k_row_stride = a.v_row_stride = ldkv;
+    a.o_row_stride = D;
+    a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = HEAD_DIM;
+    a.cu_q = cu_self_;
+    a.cu_k = cu_k;
+    a.B = B_;
+    a.H = H;
+    a.head_dim = HEAD_DIM;
+    a.max_q = T_;
+    a.max_k = max_k;
+    a.scale = 1.0f / sqrtf((float)HEAD_DIM);
+    a.max_score = kQKNormScoreBound;
+    a.split_ws = attn_ws_;
+    a.split_ws_bytes = attn_ws_bytes_;
+    return attn_fwd(a, s);
+  };
+  auto qk_norm = [&](long ldx, int heads, int rope_heads) -> int {
+    RopeNormParams rn;
+    rn.x = qkv_;
+    rn.ldx = ldx;
+    rn.rows = M_;
+    rn.heads = heads;
+    rn.rope_heads = rope_heads;
+    if (rope_heads > 0) {
+      rn.cos = cos_;
+      rn.sin = sin_;
+      rn.tokens_per_seq = T_;
+    }
+    return rope_qknorm(rn, s);
+  };
+  // --- self attention ---
+  if (norm8(b.norm1, shift_sa, scale_sa)) return 1;
+  if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
+  if (g8(nbuf8_, nbuf8_s_, q.qkv, q.qkv_s, 3L * D, 3 * D, D, b.qkv_b, EPI8_STORE_BF16, qkv_, 3L * D, nullptr))
+    return 1;
+  if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
+  if (qk_norm(3L * D, 2 * H, 2 * H)) return 1;
+  if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
+  if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, T_)) return 1;
+  if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
+  if (quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
+  if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa)) return 1;
+  // --- cross attention ---
+  if (b.cross) {
+    if (norm8(b.norm2, shift_ca, scale_ca)) return 1;
+    if (g8(nbuf8_, nbuf8_s_, q.cq, q.cq_s, D, D, D, b.cq_b, EPI8_STORE_BF16, qkv_, D, nullptr)) return 1;
+    if (qk_norm(D, H, 0)) return 1;
+    if (attn(qkv_, D, ctx_kv_[blk], ctx_kv_[blk] + D, 2L * D, cu_ctx_, ctx_max_len_)) return 1;
+    if (quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
+    if (g8(obuf8_, obuf8_s_, q.cproj, q.cproj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_ca)) return 1;
+  }
+  // --- SwiGLU MLP ---
+  if (norm8(b.norm3, shift_mlp, scale_mlp)) return 1;
+  if (probe_begin(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
+  if (g8(nbuf8_, nbuf8_s_, q.gu, q.gu_s, 2L * F, 2 * F, D, nullptr, EPI8_SWIGLU_FP8, hbuf8_, F, nullptr)) return 1;
+  if (probe_end(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
+  if (probe_begin(s, FLITE_PROBE_GEMM_DOWN)) return 1;
+  if (g8(hbuf8_, hbuf8_s_, q.down, q.down_s, D, D, F, nullptr, EPI8_RESID_F32, x_, D, gate_mlp)) return 1;
+  if (probe_end(s, FLITE_PROBE_GEMM_DOWN)) return 1;
+  return 0;
+}
+
 int DitEngine::set_probe(int kind, int max_pairs) {
   for (hipEvent_t e : probe_ev_) hipEventDestroy(e);
   probe_ev_.clear();
@@ -601,7 +793,7 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
   const long mseg = (long)t_row_step * mod_t_stride_;
   for (int i = 0; i < cfg.depth; ++i) {
     const float* mod = mod_ + (long)t_row0 * mod_t_stride_ + (cfg.per_block_adaln ? (long)i * 9 * D : 0);
-    if (run_block(s, i, mod, mseg)) return 1;
+    if (fp8_ ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg)) return 1;
   }
   // final stage (model.py:575-581): drop registers, RMSNorm (fp32 weight multiply), modulate, project
   {

@@ -8,6 +8,7 @@
 
 #include "../../include/flite.h"
 #include "common.h"
+#include "fp8.h"
 #include "kernels.h"
 
 namespace flite {
@@ -46,6 +47,9 @@ class DitEngine {
   int sample(hipStream_t s, float* acc, int Bi, int n_steps, const float* t_host, const float* dt_host,
              float guidance, int use_cfg, int apg, float apg_thr, int use_graph);
 
+  // fp8 mode (flite_dit_enable_fp8): MXFP8 copies of the block GEMM weights + fp8 activations
+  int enable_fp8(hipStream_t s, bool on);
+
   const flite_dit_config cfg;
   int D, H, F, R, P, C;
 
@@ -62,6 +66,9 @@ class DitEngine {
   int probe_n_ = 0;
 
   int run_block(hipStream_t s, int blk, const float* mod, long mseg);
+  int run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg);
+  int alloc_fp8_act();
+  void free_fp8_weights();
   int alloc(void** p, size_t bytes);
   void free_ws();
   void drop_graph();
@@ -95,6 +102,17 @@ class DitEngine {
   float* apg_scratch_ = nullptr;
   long mod_t_stride_ = 0;
   int nt_ = 0;
+  // fp8 mode
+  struct Fp8W {
+    uint8_t *qkv = nullptr, *qkv_s = nullptr, *proj = nullptr, *proj_s = nullptr, *cq = nullptr, *cq_s = nullptr;
+    uint8_t *cproj = nullptr, *cproj_s = nullptr, *gu = nullptr, *gu_s = nullptr, *down = nullptr, *down_s = nullptr;
+  };
+  bool fp8_ = false;
+  std::vector<Fp8W> w8_;
+  std::vector<void*> w8_allocs_;
+  uint8_t *nbuf8_ = nullptr, *nbuf8_s_ = nullptr, *obuf8_ = nullptr, *obuf8_s_ = nullptr;
+  uint8_t *hbuf8_ = nullptr, *hbuf8_s_ = nullptr;
+  long mpad_ = 0;
   // graph cache
   hipStream_t gstream_ = nullptr;
   hipGraphExec_t gexec_ = nullptr;

@@ -3,6 +3,7 @@
 #include <math.h>
 
 #include "common.h"
+#include "fp8.h"
 #include "kernels.h"
 
 namespace flite {
@@ -16,7 +17,30 @@ namespace {
 // then `norm_x * (1 + scale) + shift` (model.py:284,293,300,580). Computed in fp32, one rounding.
 // One wave per output row; the input row of output row m is (m / in_seg) * in_stride + in_off + m % in_seg.
 // ------------------------------------------------------------------------------------------------
-template <bool IN_BF16, int NCH>
+// 4 consecutive outputs o of row m at column n: bf16, or (OUT8) MXFP8 -- the 8 lanes of an aligned group hold the
+// 32 columns of one scale block (both norm kernels put 4 consecutive columns on consecutive lanes).
+template <bool OUT8>
+__device__ __forceinline__ void norm_store4(const NormModParams& p, long m, int n, const float (&o)[4]) {
+  if constexpr (OUT8) {
+    float amax = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+    const int e = mx_exp(amax);
+    *(unsigned*)(p.y8 + m * p.ldy + n) = pack4_fp8(o, mx_inv(e));
+    if ((n & 31) == 0) {
+      const int blk = n >> 5;
+      p.ysc[((long)(blk >> 2) * p.ysc_rows_pad + m) * 4 + (blk & 3)] = (uint8_t)(e + 127);
+    }
+  } else {
+    u32x2 st;
+    st.x = pack2bf(o[0], o[1]);
+    st.y = pack2bf(o[2], o[3]);
+    *(u32x2*)(p.y + m * p.ldy + n) = st;
+  }
+}
+
+template <bool IN_BF16, int NCH, bool OUT8 = false>
 __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(NormModParams p) {
   const int lane = threadIdx.x & 63;
   const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -55,7 +79,6 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(NormModParams p) {
   const float r = rsqrtf(ss / (float)D + p.eps);
   const float* shift = p.shift ? p.shift + seg * p.mod_seg_stride : nullptr;
   const float* scale = p.scale ? p.scale + seg * p.mod_seg_stride : nullptr;
-  bf16_t* yr = p.y + m * p.ldy;
 #pragma unroll
   for (int c = 0; c < nch; ++c) {
     const int n = c * 256 + lane * 4;
@@ -73,10 +96,7 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(NormModParams p) {
     if (shift) sh = *(const f32x4*)(shift + n);
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = v[4 * c + j] * r * wgt[j] * (1.f + sc[j]) + sh[j];
-    u32x2 st;
-    st.x = pack2bf(o[0], o[1]);
-    st.y = pack2bf(o[2], o[3]);
-    *(u32x2*)(yr + n) = st;
+    norm_store4<OUT8>(p, m, n, o);
   }
 }
 
@@ -84,7 +104,7 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(NormModParams p) {
 // Thread t holds elements q*1024 + 4t .. +3 (q < NQ): 12 fp32 registers of x instead of 48, so 8 waves per
 // SIMD stay resident and every wave has all of its row loads in flight at once; the row sum of squares is
 // a wave reduction plus 4 partials through LDS.
-template <bool IN_BF16, int NQ>
+template <bool IN_BF16, int NQ, bool OUT8 = false>
 __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
   __shared__ float part[4];
   const int t = threadIdx.x;
@@ -141,17 +161,13 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
   __syncthreads();
   ss = part[0] + part[1] + part[2] + part[3];
   const float r = rsqrtf(ss / (float)(1024 * NQ) + p.eps);
-  bf16_t* yr = p.y + m * p.ldy;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const int n = q * 1024 + t * 4;
     float o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = v[4 * q + j] * r * wgt[q][j] * (1.f + sc[q][j]) + sh[q][j];
-    u32x2 st;
-    st.x = pack2bf(o[0], o[1]);
-    st.y = pack2bf(o[2], o[3]);
-    *(u32x2*)(yr + n) = st;
+    norm_store4<OUT8>(p, m, n, o);
   }
 }
 
@@ -478,6 +494,24 @@ int grid_for(long total, int per_block = 256) {
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   FLITE_REQUIRE(p.ldx % 4 == 0 && p.ldy % 4 == 0, "rmsnorm: strides must be multiples of 4");
   if (p.rows <= 0) return 0;
+  if (p.y8 != nullptr) {  // MXFP8 output (fp8 DiT path): fp32 input rows only
+    FLITE_REQUIRE(!in_bf16 && p.ysc != nullptr && p.ysc_rows_pad >= mx_rows_pad(p.rows) && p.D % 128 == 0 &&
+                      p.ldy % 16 == 0,
+                  "rmsnorm(fp8 out): fp32 input, scales for the padded rows, D % 128, 16-B row stride");
+    if (p.D == 3072) {
+      hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, true>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
+    } else {
+      const int grid8 = (int)((p.rows + 3) / 4);
+      switch (p.D / 256) {
+        case 1: hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 1, true>), dim3(grid8), dim3(256), 0, s, p); break;
+        case 2: hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 2, true>), dim3(grid8), dim3(256), 0, s, p); break;
+        case 4: hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 4, true>), dim3(grid8), dim3(256), 0, s, p); break;
+        default: FLITE_REQUIRE(false, "rmsnorm(fp8 out): D must be 256, 512, 1024 or 3072");
+      }
+    }
+    FLITE_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
   if (p.D == 3072 && p.rows < (1L << 31)) {  // the DiT width: one workgroup per row
     if (in_bf16)
       hipLaunchKernelGGL((rmsnorm_mod_row_kernel<true, 3>), dim3((unsigned)p.rows), dim3(256), 0, s, p);

@@ -1,0 +1,65 @@
+// MXFP8 helpers and the fp8 GEMM interface (gfx950). See fp8.hip for the format and the scale layout.
+#pragma once
+#include "common.h"
+
+namespace flite {
+
+// E8M0 exponent of a block with absolute maximum `amax`: ceil(log2(amax / 448)) in [-127, 126]
+// (amax * (1/448) is one fp32 multiply, RNE; the oracle does the same multiply).
+__device__ __forceinline__ int mx_exp(float amax) {
+  const unsigned b = __float_as_uint(amax * (1.0f / 448.0f));
+  const int e = (int)((b >> 23) & 0xff) - 127 + ((b & 0x7fffffu) ? 1 : 0);
+  return e < -127 ? -127 : (e > 126 ? 126 : e);
+}
+// 2^-e (exact; e in [-127, 126])
+__device__ __forceinline__ float mx_inv(int e) { return __uint_as_float((unsigned)(127 - e) << 23); }
+
+// 4 floats * inv -> 4 OCP e4m3fn bytes (RNE), saturated to +-448 first
+__device__ __forceinline__ unsigned pack4_fp8(const float* x, float inv) {
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = fminf(fmaxf(x[j] * inv, -448.f), 448.f);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], w, true);
+  return (unsigned)w;
+}
+
+// fp8 GEMM: C[M,N] = dequant(A8)[M,K] . dequant(W8)[N,K]^T with MX block scales; fp32 accumulate.
+//   A8 / W8: e4m3 bytes, row stride lda / ldw bytes; As / Ws: scales [K/128][a_rows_pad / w_rows_pad][4].
+enum GemmFp8Epilogue {
+  EPI8_STORE_BF16 = 0,  // out_bf16[m][n] = acc + bias[n]
+  EPI8_RESID_F32 = 2,   // out_f32[m][n] += gate[seg(m)][n] * (acc + bias[n])
+  EPI8_SWIGLU_FP8 = 4,  // W8 = gate|up interleaved in 16-row sub-tiles (N = 2F): out8[m][f] = MX(silu(g) * u),
+                        // scales to out_sc [F/128][out_rows_pad][4]
+};
+
+struct GemmFp8Params {
+  const uint8_t* A = nullptr;
+  long lda = 0;
+  const uint8_t* As = nullptr;
+  long a_rows_pad = 0;
+  const uint8_t* W = nullptr;
+  long ldw = 0;
+  const uint8_t* Ws = nullptr;
+  long w_rows_pad = 0;
+  const bf16_t* bias = nullptr;
+  void* out = nullptr;  // bf16 / fp32 / fp8 bytes (row stride ldo elements; bytes for fp8)
+  long ldo = 0;
+  uint8_t* out_sc = nullptr;
+  long out_rows_pad = 0;
+  const float* gate = nullptr;
+  long gate_seg_stride = 0;
+  int rows_per_seg = 1;
+  int M = 0, N = 0, K = 0;
+};
+
+int gemm_fp8(const GemmFp8Params& p, int epi, hipStream_t s);
+int quant_rows_fp8(const bf16_t* src, long ld_src, long rows, int K, uint8_t* dst, long ld_dst, uint8_t* scales,
+                   long rows_pad, hipStream_t s);
+int quant_gateup_fp8(const bf16_t* gate, const bf16_t* up, long ld_src, int F, int K, uint8_t* dst, uint8_t* scales,
+                     hipStream_t s);
+
+// rows rounded up for the scale arrays (the GEMM stages scales for 256-row tiles)
+inline long mx_rows_pad(long rows) { return (rows + 255) / 256 * 256; }
+
+}  // namespace flite

@@ -95,6 +95,11 @@ struct NormModParams {
   // input row mapping: in_row = (m / in_seg) * in_stride + in_off + m % in_seg (in_seg = 0: identity);
   // the modulation segment of output row m is m / in_seg (0 when in_seg == 0)
   long in_seg = 0, in_stride = 0, in_off = 0;
+  // MXFP8 output instead of y (fp8 DiT path): e4m3 rows (stride ldy bytes) + k-tile-major block scales
+  // [D/128][ysc_rows_pad][4] (fp8.hip)
+  uint8_t* y8 = nullptr;
+  uint8_t* ysc = nullptr;
+  long ysc_rows_pad = 0;
 };
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s);
 

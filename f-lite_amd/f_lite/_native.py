@@ -84,9 +84,19 @@ SIGNATURES = {
     "flite_vae_decode_uint8": (_i, [_vp, _vp, _vp, _i, _vp, _f, _f]),
     "flite_vae_prepare_tiled": (_i, [_vp, _i, _i, _i, _i, _f]),
     "flite_vae_decode_tiled_uint8": (_i, [_vp, _vp, _vp, _i, _vp, _f, _f]),
+    "flite_quant_fp8_rows": (_i, [_vp, _vp, _l, _l, _i, _vp, _l, _vp, _l]),
+    "flite_quant_fp8_gateup": (_i, [_vp, _vp, _vp, _l, _i, _i, _vp, _vp]),
+    "flite_gemm_fp8": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _l, _vp, _l, _vp, _i, _vp, _l, _vp, _l, _vp, _l,
+                            _i]),
+    "flite_rmsnorm_modulate_fp8": (_i, [_vp, _vp, _l, _vp, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
+    "flite_dit_enable_fp8": (_i, [_vp, _vp, _i]),
     "flite_dit_set_probe": (_i, [_vp, _i, _i]),
     "flite_dit_read_probe": (_i, [_vp, ctypes.POINTER(_f), _i, ctypes.POINTER(_i)]),
 }
+
+EPI8_STORE_BF16 = 0
+EPI8_RESID_F32 = 2
+EPI8_SWIGLU_FP8 = 4
 
 PROBE_GEMM_GATEUP = 0
 PROBE_ATTN_SELF = 1
@@ -294,6 +304,73 @@ def cfg_euler_(acc, uncond, cond, guidance, dt, use_cfg=True):
     return acc
 
 
+# ------------------------------------------------------------------------------------------------
+# MXFP8 (include/flite.h: e4m3 elements, one E8M0 scale per 32 K elements, scales [K/128][rows_pad][4])
+# ------------------------------------------------------------------------------------------------
+def mx_rows_pad(rows: int) -> int:
+    return (rows + 255) // 256 * 256
+
+
+def quant_fp8_rows(x: torch.Tensor, rows_pad=None):
+    """bf16 [rows, K] -> (fp8 bytes uint8 [rows, K], scales uint8 [K/128, rows_pad, 4])."""
+    require_gpu(x, "x", torch.bfloat16, contiguous=False)
+    rows, K = x.shape
+    rp = rows_pad or mx_rows_pad(rows)
+    q = torch.empty(rows, K, device=x.device, dtype=torch.uint8)
+    sc = torch.zeros(K // 128, rp, 4, device=x.device, dtype=torch.uint8)
+    check(load().flite_quant_fp8_rows(stream_ptr(x.device), x.data_ptr(), x.stride(0), rows, K, q.data_ptr(), K,
+                                      sc.data_ptr(), rp), "flite_quant_fp8_rows")
+    return q, sc
+
+
+def quant_fp8_gateup(gate: torch.Tensor, up: torch.Tensor):
+    """gate/up [F, K] bf16 -> (fp8 [2F, K] interleaved in 16-row sub-tiles, scales [K/128, 2F, 4])."""
+    F, K = gate.shape
+    q = torch.empty(2 * F, K, device=gate.device, dtype=torch.uint8)
+    sc = torch.zeros(K // 128, 2 * F, 4, device=gate.device, dtype=torch.uint8)
+    check(load().flite_quant_fp8_gateup(stream_ptr(gate.device), gate.data_ptr(), up.data_ptr(), gate.stride(0), F, K,
+                                        q.data_ptr(), sc.data_ptr()), "flite_quant_fp8_gateup")
+    return q, sc
+
+
+def gemm_fp8(a8, a_sc, w8, w_sc, bias=None, *, out=None, epilogue=EPI8_STORE_BF16, out_sc=None, gate=None,
+             gate_seg_stride=0, rows_per_seg=1):
+    """C = dequant(a8) . dequant(w8)^T on the MXFP8 MFMA. a8 [M, K] / w8 [N, K] uint8 with scales from
+    quant_fp8_rows (w8/w_sc of the SwiGLU epilogue from quant_fp8_gateup, N = 2F)."""
+    lib = load()
+    M, K = a8.shape
+    N = w8.shape[0]
+    if epilogue == EPI8_SWIGLU_FP8:
+        if out is None:
+            out = torch.empty(M, N // 2, device=a8.device, dtype=torch.uint8)
+        if out_sc is None:
+            out_sc = torch.zeros(N // 2 // 128, mx_rows_pad(M), 4, device=a8.device, dtype=torch.uint8)
+    elif out is None:
+        out = torch.empty(M, N, device=a8.device, dtype=torch.bfloat16 if epilogue == EPI8_STORE_BF16 else torch.float32)
+    for t, n in ((a8, "a8"), (a_sc, "a_scales"), (w8, "w8"), (w_sc, "w_scales"), (out, "out")):
+        require_gpu(t, n, contiguous=False)
+    check(lib.flite_gemm_fp8(stream_ptr(a8.device), M, N, K, a8.data_ptr(), a8.stride(0), a_sc.data_ptr(),
+                             a_sc.shape[1], w8.data_ptr(), w8.stride(0), w_sc.data_ptr(), w_sc.shape[1], _ptr(bias),
+                             epilogue, out.data_ptr(), out.stride(0), _ptr(out_sc),
+                             out_sc.shape[1] if out_sc is not None else 0, _ptr(gate), gate_seg_stride, rows_per_seg),
+          "flite_gemm_fp8")
+    return (out, out_sc) if epilogue == EPI8_SWIGLU_FP8 else out
+
+
+def rmsnorm_modulate_fp8(x, w=None, shift=None, scale=None, seg_rows=0, eps=1e-6):
+    """RMSNorm + modulate of fp32 rows to MXFP8: (y8 uint8 [rows, D], scales [D/128, rows_pad, 4])."""
+    require_gpu(x, "x", torch.float32, contiguous=False)
+    rows, D = x.shape
+    rp = mx_rows_pad(rows)
+    y8 = torch.empty(rows, D, device=x.device, dtype=torch.uint8)
+    sc = torch.zeros(D // 128, rp, 4, device=x.device, dtype=torch.uint8)
+    check(load().flite_rmsnorm_modulate_fp8(stream_ptr(x.device), x.data_ptr(), x.stride(0), y8.data_ptr(), D,
+                                            sc.data_ptr(), rp, _ptr(w), _ptr(shift), _ptr(scale),
+                                            shift.stride(0) if shift is not None and shift.dim() == 2 else 0,
+                                            seg_rows, rows, D, eps), "flite_rmsnorm_modulate_fp8")
+    return y8, sc
+
+
 def gather_rows(src, idx, out=None):
     lib = load()
     n = idx.numel()
@@ -347,6 +424,9 @@ class DitEngine:
                                          x.shape[0], t_row0, t_row_step, out.data_ptr(),
                                          int(out.dtype == torch.bfloat16)), "flite_dit_forward")
         return out
+
+    def enable_fp8(self, on: bool = True, device=None):
+        check(self.lib.flite_dit_enable_fp8(self.h, stream_ptr(device), int(bool(on))), "flite_dit_enable_fp8")
 
     def set_probe(self, kind: int, max_pairs: int = 4096):
         check(self.lib.flite_dit_set_probe(self.h, kind, max_pairs), "flite_dit_set_probe")

@@ -164,6 +164,7 @@ class DiT(nn.Module):
         nn.init.zeros_(self.final_proj.bias)
         self._engine = None
         self._bound = None
+        self._fp8 = False
 
     # ------------------------------------------------------------------ construction helpers
     @classmethod
@@ -291,7 +292,18 @@ class DiT(nn.Module):
             for n, p in params:
                 self._engine.bind(n, p.data)
             self._bound = sig
+            if self._fp8:  # rebinding dropped the engine's fp8 copies: requantise
+                self._engine.enable_fp8(True, self.device)
         return self._engine
+
+    def enable_fp8(self, enabled: bool = True):
+        """BASELINE.json configs[4]: run every block GEMM (qkv, proj, cross q / proj, SwiGLU gate-up, down) on
+        MXFP8 weights and activations (OCP e4m3, E8M0 scale per 32 K elements) on the gfx950 block-scaled MFMA.
+        The bf16 parameters stay the source of truth; the engine quantises them once. No reference counterpart
+        (the reference runs bf16 only)."""
+        self._fp8 = bool(enabled)
+        self.engine().enable_fp8(self._fp8, self.device)
+        return self
 
     # ------------------------------------------------------------------ forward
     @torch.no_grad()

@@ -110,6 +110,35 @@ int flite_rmsnorm_modulate(void* stream, const void* x, int x_is_bf16, long ldx,
 int flite_rope_qknorm(void* stream, void* x, long ldx, long rows, int heads, int rope_heads, const float* cos_t,
                       const float* sin_t, long tokens_per_seq, float eps);
 
+/* ---------------------------------------------------------------------------------------------
+ * MXFP8 (BASELINE.json configs[4]: fp8 weights + activations). Elements OCP e4m3fn, one E8M0 scale per 32
+ * consecutive K elements: e = ceil(log2(amax/448)), q = RNE(clamp(x * 2^-e, +-448)). Scale arrays are
+ * "k-tile major": scales[K/128][rows_pad][4] bytes (rows_pad a multiple of 256, >= rows; pad rows are never
+ * read back). The reference has no fp8 path: these replace the nn.Linear calls of model.py:151-156 and
+ * LigerSwiGLUMLP (model.py:261-267) in the fp8 configuration.
+ * ------------------------------------------------------------------------------------------- */
+#define FLITE_EPI8_STORE_BF16 0  /* out_bf16[m][n]  = A.W^T + bias                                   */
+#define FLITE_EPI8_RESID_F32 2   /* out_f32[m][n]  += gate[m/rows_per_seg][n] * (A.W^T + bias)       */
+#define FLITE_EPI8_SWIGLU_FP8 4  /* out_fp8[m][f]   = MX(silu(A.Wg^T) * (A.Wu^T)), W = gate|up interleaved in
+                                    16-row sub-tiles (flite_quant_fp8_gateup), N = 2F; scales to out_scales */
+
+/* bf16 rows [rows, K] (row stride ld_src elements) -> fp8 [rows, K] (row stride ld_dst bytes) + scales. */
+int flite_quant_fp8_rows(void* stream, const void* src, long ld_src, long rows, int K, void* dst, long ld_dst,
+                         void* scales, long rows_pad);
+/* SwiGLU weights gate_proj/up_proj [F, K] -> one fp8 [2F, K] matrix with gate and up rows interleaved in 16-row
+ * sub-tiles (the pairing of the fused SwiGLU epilogue) + scales [K/128][2F][4]. */
+int flite_quant_fp8_gateup(void* stream, const void* gate, const void* up, long ld_src, int F, int K, void* dst,
+                           void* scales);
+/* MXFP8 GEMM C = A8 . W8^T on the block-scaled MFMA (fp32 accumulate). K % 128 == 0; lda, ldw % 16 == 0. */
+int flite_gemm_fp8(void* stream, int M, int N, int K, const void* A8, long lda, const void* a_scales,
+                   long a_rows_pad, const void* W8, long ldw, const void* w_scales, long w_rows_pad,
+                   const void* bias, int epilogue, void* out, long ldo, void* out_scales, long out_rows_pad,
+                   const float* gate, long gate_seg_stride, int rows_per_seg);
+/* flite_rmsnorm_modulate with MXFP8 output (fp32 x): y8 [rows, dim] bytes (row stride ldy) + scales. */
+int flite_rmsnorm_modulate_fp8(void* stream, const float* x, long ldx, void* y8, long ldy, void* y_scales,
+                               long rows_pad, const void* w, const float* shift, const float* scale,
+                               long mod_seg_stride, long seg_rows, long rows, int dim, float eps);
+
 /* Row gather dst[i] = src[idx[i]] (bf16 rows of `cols`, cols % 8 == 0): the context compaction of
  * prepare_flash_attention_inputs (model.py:61-62) for a ragged context_attn_mask. idx: device int32 [n]. */
 int flite_gather_rows(void* stream, const void* src, void* dst, const int* idx, long n, int cols);
@@ -186,6 +215,14 @@ int flite_dit_sample(flite_dit* dit, void* stream, float* acc, int n_img, int n_
  */
 int flite_cfg_euler(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
                     float dt, int use_cfg);
+/*
+ * fp8 mode (BASELINE.json configs[4]): enable=1 quantises every bound block GEMM weight (qkv, proj, cross q /
+ * proj, SwiGLU gate|up, down) once into engine-owned MXFP8 copies and runs those GEMMs on the block-scaled fp8
+ * MFMA with MXFP8 activations (RMSNorm+modulate, attention output and SwiGLU output quantised where they are
+ * produced). Attention, norms, RoPE, the residual stream and the small GEMMs stay bf16/fp32. enable=0 returns to
+ * the bf16 path. Re-binding a weight drops the fp8 copies; call again to requantise.
+ */
+int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable);
 
 /*
  * 3x3 convolution, padding 1, stride 1 (nn.Conv2d of the diffusers VAE decoder), optionally preceded by a

@@ -80,6 +80,43 @@ def apply_rotary_emb(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> t
     return torch.cat([x1 * cos + x2 * sin, x1 * (-sin) + x2 * cos], -1).to(od)
 
 
+# --------------------------------------------------------------------------------------------------
+# MXFP8 fake-quant (the fp8 configuration, BASELINE.json configs[4]; no reference counterpart: the reference runs
+# bf16 only). Restates include/flite.h / f-lite_amd/csrc/fp8.hip bit for bit: OCP e4m3fn elements, one E8M0 scale
+# per 32 consecutive elements of the last dim, e = ceil(log2(amax * (1/448))) from the fp32 bits, clamped to
+# [-127, 126]; element = RNE(clamp(x * 2^-e, +-448)).
+# --------------------------------------------------------------------------------------------------
+def _mx_exp(xb: torch.Tensor) -> torch.Tensor:
+    amax = xb.abs().amax(-1, keepdim=True)
+    a = (amax * torch.tensor(1.0 / 448.0, dtype=torch.float32)).contiguous()
+    bits = a.view(torch.int32)
+    e = ((bits >> 23) & 0xFF) - 127 + ((bits & 0x7FFFFF) != 0).to(torch.int32)
+    return e.clamp(-127, 126)
+
+
+def mx_quant(x: torch.Tensor, block: int = 32) -> torch.Tensor:
+    """MXFP8 quantise-dequantise along the last dim; returns fp32 (the values the fp8 GEMM multiplies)."""
+    shp = x.shape
+    xb = x.float().reshape(*shp[:-1], shp[-1] // block, block)
+    e = _mx_exp(xb)
+    one = torch.ones((), dtype=torch.float32)
+    q = (xb * torch.ldexp(one, -e)).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
+    return (q * torch.ldexp(one, e)).reshape(shp)
+
+
+def mx_quant_bytes(x: torch.Tensor, rows_pad: Optional[int] = None):
+    """(e4m3 bytes uint8 [rows, K], scales uint8 [K/128, rows_pad, 4]) as flite_quant_fp8_rows writes them."""
+    rows, K = x.shape
+    xb = x.float().reshape(rows, K // 32, 32)
+    e = _mx_exp(xb)
+    one = torch.ones((), dtype=torch.float32)
+    q = (xb * torch.ldexp(one, -e)).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+    rp = rows_pad or (rows + 255) // 256 * 256
+    sc = torch.zeros(K // 128, rp, 4, dtype=torch.uint8)
+    sc[:, :rows, :] = (e[..., 0] + 127).to(torch.uint8).reshape(rows, K // 128, 4).permute(1, 0, 2)
+    return q.reshape(rows, K), sc
+
+
 def attention_varlen(q, k, v, cu_q, cu_k, scale):
     """flash_attn_varlen_func: q [Lq, h, d], k/v [Lk, h, d]; fp32 softmax, output in q.dtype."""
     out = torch.empty_like(q)
@@ -142,11 +179,30 @@ PRESETS = {
 class RefDiT:
     """Functional restatement of DiT.forward; params is a state dict (fp32 values), cast to `dtype`."""
 
-    def __init__(self, cfg: DiTConfig, params: dict, dtype=torch.float32, rope_dtype=None):
+    # block GEMM weights that the fp8 configuration runs in MXFP8 (f-lite_amd/csrc/dit.cpp: run_block_fp8)
+    FP8_WEIGHTS = ("self_attn.qkv", "self_attn.proj", "cross_attn.q", "cross_attn.proj", "mlp.gate_proj",
+                   "mlp.up_proj", "mlp.down_proj")
+
+    def __init__(self, cfg: DiTConfig, params: dict, dtype=torch.float32, rope_dtype=None, fp8: bool = False):
         self.cfg = cfg
         self.dtype = dtype
         self.p = {k: v.to(dtype) for k, v in params.items()}
         self.rope_dtype = rope_dtype if rope_dtype is not None else dtype
+        # fp8: fake-quantised (MXFP8) block GEMM weights and the activations feeding them
+        self.fp8 = fp8
+        if fp8:
+            for k in list(self.p):
+                if k.startswith("blocks.") and k.endswith(".weight") and \
+                        any(("." + n + ".") in k for n in self.FP8_WEIGHTS):
+                    self.p[k] = mx_quant(self.p[k]).to(dtype)
+
+    def _q8(self, a, round_bf16=False):
+        """fp8 mode: the MXFP8 operand an activation becomes (attention outputs are bf16 tensors first)."""
+        if not self.fp8:
+            return a
+        if round_bf16:
+            a = a.to(torch.bfloat16)
+        return mx_quant(a).to(self.dtype)
 
     @classmethod
     def random(cls, cfg: DiTConfig, seed: int = 0, dtype=torch.float32, **kw):
@@ -162,7 +218,7 @@ class RefDiT:
         H = c.num_heads
         (shift_sa, scale_sa, gate_sa, shift_ca, scale_ca, gate_ca, shift_mlp, scale_mlp, gate_mlp) = mod
         n = liger_rmsnorm(x, self.p[pre + "norm1.weight"])
-        n = n * (1 + scale_sa) + shift_sa
+        n = self._q8(n * (1 + scale_sa) + shift_sa)
         qkv = self._lin(n, pre + "self_attn.qkv")
         L = qkv.shape[0]
         qkv = qkv.reshape(L, 3, H, -1).permute(1, 2, 0, 3)  # "l (k h d) -> k h l d"
@@ -173,24 +229,24 @@ class RefDiT:
         k = own_rmsnorm(k, None)
         q, k, v = (t.transpose(0, 1) for t in (q, k, v))  # "h l d -> l h d"
         hd = q.shape[-1]
-        a = attention_varlen(q, k, v, cu, cu, hd ** -0.5).reshape(L, -1)
+        a = self._q8(attention_varlen(q, k, v, cu, cu, hd ** -0.5).reshape(L, -1), round_bf16=True)
         x = x + self._lin(a, pre + "self_attn.proj", bias=False) * gate_sa
         if c.cross(i):
             n = liger_rmsnorm(x, self.p[pre + "norm2.weight"])
-            n = n * (1 + scale_ca) + shift_ca
+            n = self._q8(n * (1 + scale_ca) + shift_ca)
             q = self._lin(n, pre + "cross_attn.q").reshape(L, H, -1)
             kv = self._lin(ctx, pre + "cross_attn.context_kv")
             kv = kv.reshape(kv.shape[0], 2, H, -1).permute(1, 0, 2, 3)  # "l (k h d) -> k l h d"
             kk, vv = kv.unbind(0)
             q = own_rmsnorm(q, None)
             kk = own_rmsnorm(kk, None)
-            a = attention_varlen(q, kk, vv, cu, ctx_cu, hd ** -0.5).reshape(L, -1)
+            a = self._q8(attention_varlen(q, kk, vv, cu, ctx_cu, hd ** -0.5).reshape(L, -1), round_bf16=True)
             x = x + self._lin(a, pre + "cross_attn.proj", bias=False) * gate_ca
         n = liger_rmsnorm(x, self.p[pre + "norm3.weight"])
-        n = n * (1 + scale_mlp) + shift_mlp
+        n = self._q8(n * (1 + scale_mlp) + shift_mlp)
         g = self._lin(n, pre + "mlp.gate_proj", bias=False)
         u = self._lin(n, pre + "mlp.up_proj", bias=False)
-        hmid = F.silu(g.float()).to(u.dtype) * u
+        hmid = self._q8(F.silu(g.float()).to(u.dtype) * u)
         x = x + self._lin(hmid, pre + "mlp.down_proj", bias=False) * gate_mlp
         return x
 

@@ -1,0 +1,176 @@
+"""GPU: the MXFP8 path (BASELINE.json configs[4]: fp8 weights + activations on the gfx950 block-scaled MFMA).
+
+The reference has no fp8 path, so the oracle is a FAKE-QUANT restatement (oracle/flite_ref.py: mx_quant /
+mx_quant_bytes / RefDiT(fp8=True)): the same MXFP8 rounding applied at the same points of the fp32 forward.
+Bars:
+  - quantisation kernels (flite_quant_fp8_rows, the fp8-output RMSNorm): bit-exact e4m3 bytes and E8M0 scales;
+  - fp8 GEMM: vs an fp64 product of the dequantised operands, rel-L2 <= 1e-5 (fp32 accumulation of exact
+    fp8 x fp8 products; only the summation order differs);
+  - fp8 DiT forward: >= 30 dB PSNR vs the fake-quant oracle (quantiser inputs differ by bf16 roundings, which
+    can move an element by one e4m3 step); the distance to the un-quantised fp32 oracle is reported.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no ROCm device", allow_module_level=True)
+
+from f_lite import DiT  # noqa: E402
+from f_lite import _native as nat  # noqa: E402
+from f_lite.model import PRESETS  # noqa: E402
+from oracle import flite_ref as R  # noqa: E402
+
+DEV = "cuda"
+
+
+def dequant(q: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
+    """uint8 e4m3 [rows, K] + scales [K/128, rows_pad, 4] -> fp32."""
+    rows, K = q.shape
+    v = q.cpu().view(torch.float8_e4m3fn).float()
+    e = sc.cpu()[:, :rows, :].permute(1, 0, 2).reshape(rows, K // 32).to(torch.int32) - 127
+    return (v.reshape(rows, K // 32, 32) * torch.ldexp(torch.ones(()), e)[..., None]).reshape(rows, K)
+
+
+def psnr(a, ref):
+    mse = (a.double() - ref.double()).pow(2).mean().item()
+    return float("inf") if mse == 0 else 10 * math.log10(ref.double().abs().max().item() ** 2 / mse)
+
+
+def test_e4m3_conversion_matches_torch():
+    """v_cvt_pk_fp8_f32 on gfx950 is OCP e4m3fn with round-to-nearest-even (incl. subnormals and ties)."""
+    g = torch.Generator().manual_seed(1)
+    x = torch.cat([torch.randn(64, 1024, generator=g) * s for s in (1e-3, 0.1, 1.0, 30.0)])
+    x[0, :8] = torch.tensor([0.0, -0.0, 1e-30, 448.0, -448.0, 2 ** -9, 3 * 2 ** -10, 1.0 + 2 ** -4])
+    x = x.bfloat16()
+    q, sc = nat.quant_fp8_rows(x.to(DEV))
+    qr, scr = R.mx_quant_bytes(x.float())
+    assert torch.equal(sc.cpu()[:, : x.shape[0]], scr[:, : x.shape[0]])
+    assert torch.equal(q.cpu(), qr)
+
+
+@pytest.mark.parametrize("rows,K", [(300, 512), (8224, 3072)])
+def test_quant_rows_bit_exact(rows, K):
+    g = torch.Generator().manual_seed(rows)
+    x = (torch.randn(rows, K, generator=g) * torch.logspace(-3, 2, K)[None]).bfloat16()
+    q, sc = nat.quant_fp8_rows(x.to(DEV))
+    qr, scr = R.mx_quant_bytes(x.float())
+    assert torch.equal(q.cpu(), qr)
+    assert torch.equal(sc.cpu()[:, :rows], scr[:, :rows])
+    torch.testing.assert_close(dequant(q, sc), R.mx_quant(x.float()), rtol=0, atol=0)
+
+
+def test_rmsnorm_fp8_output():
+    rows, D, T = 600, 3072, 300
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(rows, D, generator=g) * 3
+    w = (1 + 0.1 * torch.randn(D, generator=g)).bfloat16()
+    shift = torch.randn(2, D, generator=g) * 0.1
+    scale = torch.randn(2, D, generator=g) * 0.1
+    y8, sc = nat.rmsnorm_modulate_fp8(x.to(DEV), w.to(DEV), shift.to(DEV), scale.to(DEV), seg_rows=T)
+    seg = torch.arange(rows) // T
+    ref = R.liger_rmsnorm(x, w.float()) * (1 + scale[seg]) + shift[seg]
+    got = dequant(y8, sc)
+    want = R.mx_quant(ref)
+    mism = (got != want).float().mean().item()
+    print(f"fp8 RMSNorm: {mism * 100:.4f} % of elements differ from the fake-quant oracle (rsqrt/sum order)")
+    assert mism < 1e-3
+    assert psnr(got, want) > 60
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(300, 256, 512, "resid"), (8224, 3072, 3072, "resid"),
+                                       (1000, 1536, 512, "store"), (8224, 9216, 3072, "store")])
+def test_gemm_fp8(M, N, K, epi):
+    g = torch.Generator().manual_seed(M + N)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.02).bfloat16()
+    bias = (torch.randn(N, generator=g) * 0.1).bfloat16()
+    a8, asc = nat.quant_fp8_rows(a.to(DEV))
+    w8, wsc = nat.quant_fp8_rows(w.to(DEV))
+    ref = dequant(a8, asc).double() @ dequant(w8, wsc).double().t() + bias.double()
+    if epi == "resid":
+        gate = torch.ones(1, N, device=DEV)
+        out = torch.zeros(M, N, device=DEV)
+        nat.gemm_fp8(a8, asc, w8, wsc, bias.to(DEV), out=out, epilogue=nat.EPI8_RESID_F32, gate=gate,
+                     gate_seg_stride=0, rows_per_seg=M)
+        err = (out.cpu().double() - ref).norm() / ref.norm()
+        assert err < 1e-5, err
+    else:
+        out = nat.gemm_fp8(a8, asc, w8, wsc, bias.to(DEV))
+        err = (out.cpu().double() - ref).norm() / ref.norm()
+        assert err < 4e-3, err  # bf16 output rounding
+
+
+def test_gemm_fp8_swiglu():
+    M, F, K = 1000, 1024, 512
+    g = torch.Generator().manual_seed(9)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    wg = (torch.randn(F, K, generator=g) * 0.05).bfloat16()
+    wu = (torch.randn(F, K, generator=g) * 0.05).bfloat16()
+    a8, asc = nat.quant_fp8_rows(a.to(DEV))
+    gu8, gusc = nat.quant_fp8_gateup(wg.to(DEV), wu.to(DEV))
+    h8, hsc = nat.gemm_fp8(a8, asc, gu8, gusc, epilogue=nat.EPI8_SWIGLU_FP8)
+    ad = dequant(a8, asc).double()
+    gd = ad @ R.mx_quant(wg.float()).double().t()
+    ud = ad @ R.mx_quant(wu.float()).double().t()
+    h = (torch.nn.functional.silu(gd) * ud).float()
+    got = dequant(h8, hsc)
+    want = R.mx_quant(h)
+    p = psnr(got, want)
+    mism = (got != want).float().mean().item()
+    print(f"fp8 SwiGLU GEMM: {p:.1f} dB vs fake-quant fp64; {mism * 100:.3f} % elements differ")
+    assert p > 45 and mism < 0.02
+
+
+@pytest.mark.parametrize("preset", ["tiny", "tiny_v2"])
+def test_dit_fp8_forward_vs_fake_quant_oracle(golden, preset):
+    m = DiT.random(seed=0, device=DEV, **PRESETS[preset])
+    x = golden["in.x"].bfloat16()
+    ctx = golden["in.ctx"].bfloat16()
+    t = golden["in.t"]
+    bf = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32).cpu()
+    m.enable_fp8(True)
+    out = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32).cpu()
+    m.enable_fp8(False)
+    again = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32).cpu()
+    assert torch.equal(bf, again)  # back on the bf16 path
+    with torch.no_grad():
+        fq = R.RefDiT.random(R.PRESETS[preset], dtype=torch.float32, fp8=True)(x.float(), ctx.float(), None, t)
+        f32 = R.RefDiT.random(R.PRESETS[preset], dtype=torch.float32)(x.float(), ctx.float(), None, t)
+    p_fq, p_32, p_bf = psnr(out, fq), psnr(out, f32), psnr(bf, f32)
+    print(f"{preset} fp8 forward: {p_fq:.2f} dB vs fake-quant oracle, {p_32:.2f} dB vs fp32 oracle "
+          f"(bf16 path: {p_bf:.2f} dB; fake-quant oracle vs fp32 oracle {psnr(fq, f32):.2f} dB)")
+    assert p_fq >= 30.0
+
+
+def test_dit_fp8_sampling_loop_graph_equals_eager(golden):
+    from f_lite import FLitePipeline
+
+    m = DiT.random(seed=0, device=DEV, **PRESETS["tiny"]).enable_fp8(True)
+    pipe = FLitePipeline(m)
+    lat = golden["pipe.in.latents"].bfloat16().to(DEV)
+    pos = golden["pipe.in.pos"].bfloat16().to(DEV)
+    run = [pipe(prompt_embeds=pos, latents=lat, height=128, width=128, num_inference_steps=4, guidance_scale=6.0,
+                output_type="latent", use_graph=gr).images.float().cpu() for gr in (False, True, True)]
+    assert torch.isfinite(run[0]).all()
+    assert torch.equal(run[0], run[1]) and torch.equal(run[1], run[2])
+
+
+def test_10b_fp8_full_size_forward():
+    """The configs[4] model at the reference's default 1344x896 (T = 4720), full depth: fp8 vs the bf16 path."""
+    m = DiT.random(seed=0, device=DEV, **PRESETS["10b"])
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 16, 112, 168, generator=g).bfloat16().to(DEV)
+    ctx = torch.randn(2, 512, 4096, generator=g).bfloat16().to(DEV)
+    t = torch.tensor([0.75, 0.75]).bfloat16().to(DEV)
+    bf = m(x, ctx, None, t, output_dtype=torch.float32).cpu()
+    m.enable_fp8(True)
+    f8 = m(x, ctx, None, t, output_dtype=torch.float32).cpu()
+    f8b = m(x, ctx, None, t, output_dtype=torch.float32).cpu()
+    assert torch.isfinite(f8).all() and torch.equal(f8, f8b)
+    p = psnr(f8, bf)
+    print(f"10B 1344x896 full-depth forward: fp8 vs bf16 path {p:.2f} dB")
+    assert p > 15.0
