@@ -199,6 +199,8 @@ def main():
     ap.add_argument("--vae-tiling", action="store_true",
                     help="pipe.enable_vae_tiling() as generate.py:77-78 does (tiled decode above 1024 px)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--images-per-gpu", type=int, default=1,
+                    help="images per bench step and GPU, sampled as ONE batch (num_images_per_prompt; M = 2 x B x T)")
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE configs[4]: block GEMMs on MXFP8 weights + activations (block-scaled fp8 MFMA)")
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
@@ -250,16 +252,21 @@ def main():
 
     lh, lw = args.height // 8, args.width // 8
 
-    def latents_for(i):
-        lat = torch.empty(1, 16, lh, lw, device=dev, dtype=torch.bfloat16)
-        return nat.init_param_(lat, f"synthetic.latents.{i}", seed=2, std=1.0)
+    BI = args.images_per_gpu
+
+    def latents_for(i):  # step i of this rank: images i * BI .. i * BI + BI - 1
+        lats = []
+        for j in range(i * BI, i * BI + BI):
+            lat = torch.empty(1, 16, lh, lw, device=dev, dtype=torch.bfloat16)
+            lats.append(nat.init_param_(lat, f"synthetic.latents.{j}", seed=2, std=1.0))
+        return torch.cat(lats)
 
     out_type = "latent" if vae is None else "uint8"
 
     def one_image(i):
         return pipe(prompt_embeds=ctx, latents=latents_for(i), height=args.height, width=args.width,
                     num_inference_steps=args.sample_steps, guidance_scale=args.guidance, output_type=out_type,
-                    use_graph=not args.no_graph).images
+                    num_images_per_prompt=BI, use_graph=not args.no_graph).images
 
     mine = image_indices(world * (args.steps + args.warmup), rank, world)  # image i -> GPU i mod N
     for w in range(args.warmup):
@@ -287,7 +294,7 @@ def main():
         eng.set_probe(kinds[args.probe], 4 * cfg["depth"] * args.sample_steps)
         pipe(prompt_embeds=ctx, latents=latents_for(rank), height=args.height, width=args.width,
              num_inference_steps=args.sample_steps, guidance_scale=args.guidance, output_type=out_type,
-             use_graph=False)
+             num_images_per_prompt=BI, use_graph=False)
         torch.cuda.synchronize()
         probe_ms = eng.read_probe(8192)
         eng.set_probe(-1, 0)
@@ -297,20 +304,20 @@ def main():
         return
 
     ms_per_step = elapsed / args.steps * 1000.0
-    value = world * args.steps / elapsed
+    value = world * args.steps * BI / elapsed
     f_step, f_once = dit_flops(cfg, args.height, args.width, args.sample_steps)
     f_vae = vae_flops(args.height, args.width) if vae is not None else 0.0
     f_image = args.sample_steps * 2 * f_step + 2 * f_once + f_vae
     D = cfg["hidden_size"]
     F = int(D * cfg["mlp_ratio"])
     T = 16 + (args.height // 16) * (args.width // 16)
-    M = 2 * T
+    M = 2 * BI * T
     per_launch = {
         "gateup": (2.0 * M * 2 * F * D, "SwiGLU gate/up GEMM (M=%d, N=%d, K=%d)" % (M, 2 * F, D)),
         "down": (2.0 * M * D * F, "down GEMM + gated residual (M=%d, N=%d, K=%d)" % (M, D, F)),
         "qkv": (2.0 * M * 3 * D * D, "qkv GEMM (M=%d, N=%d, K=%d)" % (M, 3 * D, D)),
-        "attn": (2 * 4.0 * T * T * D, "self-attention (B=2, H=%d, T=%d, hd=256)" % (cfg["num_heads"], T)),
-        "step": (2.0 * f_step, "one CFG-batched denoise step"),
+        "attn": (2 * BI * 4.0 * T * T * D, "self-attention (B=%d, H=%d, T=%d, hd=256)" % (2 * BI, cfg["num_heads"], T)),
+        "step": (2.0 * BI * f_step, "one CFG-batched denoise step"),
     }
     roofline = None
     if probe_ms:
@@ -365,7 +372,7 @@ def main():
             args.model.upper(), "model_v2 layout" if cfg["per_block_adaln"] else "model.py layout",
             args.width, args.height, args.sample_steps, args.guidance,
             "VAE decode to uint8" if vae is not None else "latents only (no VAE)"),
-                   "images_per_gpu_per_step": 1, "cfg_batch": 2, "parallelism": "replica dp%d" % world,
+                   "images_per_gpu_per_step": BI, "cfg_batch": 2, "parallelism": "replica dp%d" % world,
                    "hipgraph": not args.no_graph, "vae_tiling": bool(args.vae_tiling)},
         "distributed": {"world_size": world, "backend": "nccl (RCCL over xGMI)" if world > 1 else "none",
                         "collectives": "one broadcast of the [1,512,4096] context from rank 0 before the loop",
