@@ -15,6 +15,13 @@ constexpr int HEAD_DIM = 256;
 // (+ bf16 rounding), so |q.k| / sqrt(256) <= 16; 16.5 leaves margin for the rounding of q and k.
 constexpr float kQKNormScoreBound = 16.5f;
 
+// RoPE + QK-norm fused into the qkv / cross-q GEMM epilogue (gemm.hip EPI_QKV_NORM_BF16); FLITE_NO_QK_FUSION=1
+// runs the separate rope_qknorm kernel instead (A/B switch for measurements)
+bool fuse_qk_norm() {
+  static const bool on = getenv("FLITE_NO_QK_FUSION") == nullptr;
+  return on;
+}
+
 bool parse_block(const std::string& name, int* idx, std::string* rest) {
   if (name.rfind("blocks.", 0) != 0) return false;
   const size_t dot = name.find('.', 7);
@@ -439,11 +446,16 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.M = (int)M_;
     g.N = 3 * D;
     g.K = D;
+    // RoPE + QK-norm of the q and k heads ("(k h d)" layout, model.py:163) in the GEMM epilogue
+    g.rope_cos = cos_;
+    g.rope_sin = sin_;
+    g.rope_tokens = T_;
+    g.rope_cols = g.norm_cols = 2 * D;
     if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
-    if (gemm(g, EPI_STORE_BF16, s)) return 1;
+    if (gemm(g, fuse_qk_norm() ? EPI_QKV_NORM_BF16 : EPI_STORE_BF16, s)) return 1;
     if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
   }
-  {
+  if (!fuse_qk_norm()) {
     RopeNormParams rn;
     rn.x = qkv_;
     rn.ldx = 3L * D;
@@ -495,14 +507,17 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.M = (int)M_;
     g.N = D;
     g.K = D;
-    if (gemm(g, EPI_STORE_BF16, s)) return 1;
-    RopeNormParams rn;
-    rn.x = qkv_;
-    rn.ldx = D;
-    rn.rows = M_;
-    rn.heads = H;
-    rn.rope_heads = 0;
-    if (rope_qknorm(rn, s)) return 1;
+    g.norm_cols = D;  // query QK-norm (model.py:197) in the epilogue
+    if (gemm(g, fuse_qk_norm() ? EPI_QKV_NORM_BF16 : EPI_STORE_BF16, s)) return 1;
+    if (!fuse_qk_norm()) {
+      RopeNormParams rn;
+      rn.x = qkv_;
+      rn.ldx = D;
+      rn.rows = M_;
+      rn.heads = H;
+      rn.rope_heads = 0;
+      if (rope_qknorm(rn, s)) return 1;
+    }
     AttnParams a;
     a.q = qkv_;
     a.k = ctx_kv_[blk];

@@ -385,12 +385,117 @@ struct GemmCta {
     }
   }
 
+  // qkv / cross-q epilogue (EPI_QKV_NORM_BF16). A 256-column tile is exactly one head (n0 % 256 == 0). Columns
+  // [0, norm_cols) get, in fp32 and with one bf16 rounding at the end: RoPE (apply_rotary_emb, model.py:403-414:
+  // y1 = x1 c + x2 s, y2 = -x1 s + x2 c for the pairs (j, j + 128), tables of the bf16 model) on columns
+  // [0, rope_cols), then QKNorm's RMSNorm over the head (model.py:115-126,180,197). Column j and j + 128 of a row
+  // sit in waves wave_n and wave_n ^ 2 at the same lane and register, so RoPE swaps values through LDS in four
+  // passes of two 16-row blocks (64 KiB); the head's sum of squares is a 4-lane shuffle plus 4 wave partials in LDS.
+  __device__ __forceinline__ void qkv_norm_epilogue(f32x4 (&acc)[8][4], int m0, int n0, int m_base, int n_base) {
+    float bias[4][4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n_base + ni * 16 + r;
+        bias[ni][r] = (p.bias != nullptr && n < p.N) ? bf2f(p.bias[n]) : 0.f;
+      }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[mi][ni][r] += bias[ni][r];
+    const bool norm = n0 < p.norm_cols;  // tile-uniform
+    if (norm) {
+      __syncthreads();  // every wave is done with the k-tile buffers
+      if (n0 < p.rope_cols) {
+        const int pw = wave ^ 2;  // the wave holding the other half of every rotation pair
+        const bool first = wave_n < 2;
+        const int ja = (wave_n & 1) * 64 + lk * 4;  // angle index of (ni = 0, r = 0)
+        const int T = (int)p.rope_tokens;
+        int tok = min(m_base, p.M - 1) % T;  // token of block mi = 0; + 16 per block (T > 16), wrapped
+#pragma unroll
+        for (int pass = 0; pass < 4; ++pass) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni)
+              if (2 * pass + i < MI)
+                *(LDS_AS f32x4*)(lds0 + ((wave * 8 + i * 4 + ni) * 64 + lane) * 16) = acc[2 * pass + i][ni];
+          __syncthreads();
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int mi = 2 * pass + i;
+            if (mi >= MI) continue;
+            const float* ct = p.rope_cos + (long)tok * 128 + ja;
+            const float* st = p.rope_sin + (long)tok * 128 + ja;
+            tok = tok + 16 >= T ? tok + 16 - T : tok + 16;  // rows >= M compute garbage and are never stored
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+              const f32x4 other = *(const LDS_AS f32x4*)(lds0 + ((pw * 8 + i * 4 + ni) * 64 + lane) * 16);
+              const f32x4 c = *(const f32x4*)(ct + ni * 16);
+              const f32x4 sn = *(const f32x4*)(st + ni * 16);
+              f32x4 y;
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                y[r] = first ? acc[mi][ni][r] * c[r] + other[r] * sn[r] : -other[r] * sn[r] + acc[mi][ni][r] * c[r];
+              acc[mi][ni] = y;
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one 16-row block's table loads in flight at a time (registers)
+          }
+          __syncthreads();  // the next pass rewrites the exchange area
+        }
+      }
+      // per-head RMSNorm: row sum of squares = 4 lanes (lk) x 4 waves (wave_n)
+      const unsigned sums = lds0 + 65536;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        float ss = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ss += acc[mi][ni][r] * acc[mi][ni][r];
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        if (lk == 0) *(LDS_AS float*)(sums + (((wave_m * 8 + mi) * 16 + lr) * 4 + wave_n) * 4) = ss;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const f32x4 part = *(const LDS_AS f32x4*)(sums + ((wave_m * 8 + mi) * 16 + lr) * 16);
+        const float rn = rsqrtf((part[0] + part[1] + part[2] + part[3]) * (1.f / 256.f) + p.norm_eps);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[mi][ni][r] *= rn;
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m = m_base + mi * 16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int n = n_base + ni * 16;
+        if (n >= p.N) continue;
+        u32x2 w;
+        w.x = pack2bf(acc[mi][ni][0], acc[mi][ni][1]);
+        w.y = pack2bf(acc[mi][ni][2], acc[mi][ni][3]);
+        *(u32x2*)((bf16_t*)p.out + (long)m * p.ldo + n) = w;
+      }
+    }
+  }
+
   // ---- epilogue: lane holds C[m][n..n+3] for m = m_base + mi*16 + (lane&15), n = n_base + ni*16 + 4*(lane>>4)
-  __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], int m0, int n0) {
+  __device__ __forceinline__ void epilogue(f32x4 (&acc)[8][4], int m0, int n0) {
     const int m_base = m0 + wave_m * WM + lr;
     const int n_base = n0 + wave_n * 64 + lk * 4;
 
-    if constexpr (EPI == EPI_SWIGLU_BF16) {
+    if constexpr (EPI == EPI_QKV_NORM_BF16) {
+      qkv_norm_epilogue(acc, m0, n0, m_base, n_base);
+      return;
+    } else if constexpr (EPI == EPI_SWIGLU_BF16) {
       // pairs (ni=0 gate, ni=1 up), (ni=2 gate, ni=3 up) -> output column (n0/2 + wave_n*32 + pair*16 + 4*(lane>>4))
       const int F = p.N >> 1;
 #pragma unroll
@@ -713,6 +818,7 @@ int gemm_init() {
   FLITE_HIP_CHECK(set_attrs<EPI_STORE_F32>());
   FLITE_HIP_CHECK(set_attrs<EPI_RESID_F32>());
   FLITE_HIP_CHECK(set_attrs<EPI_SWIGLU_BF16>());
+  FLITE_HIP_CHECK(set_attrs<EPI_QKV_NORM_BF16>());
   {
     int dev = 0;
     FLITE_HIP_CHECK(hipGetDevice(&dev));
@@ -771,6 +877,15 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
       FLITE_REQUIRE(p.gate == nullptr || p.rows_per_seg > 0, "gemm(resid): rows_per_seg must be > 0");
       FLITE_REQUIRE(p.out_seg == 0 && p.act == 0, "gemm(resid): no row remap or activation");
       launch<EPI_RESID_F32>(p, stream);
+      break;
+    case EPI_QKV_NORM_BF16:
+      FLITE_REQUIRE(p.N % 256 == 0 && p.ldo % 4 == 0 && p.norm_cols % 256 == 0 && p.rope_cols % 256 == 0 &&
+                        p.rope_cols <= p.norm_cols && p.norm_cols <= p.N,
+                    "gemm(qkv_norm): heads of 256 columns (N, norm_cols, rope_cols multiples of 256)");
+      FLITE_REQUIRE(p.rope_cols == 0 || (p.rope_cos && p.rope_sin && p.rope_tokens > 0),
+                    "gemm(qkv_norm): RoPE tables missing");
+      FLITE_REQUIRE(p.out_seg == 0 && p.act == 0 && p.resid == nullptr, "gemm(qkv_norm): plain row layout only");
+      launch<EPI_QKV_NORM_BF16>(p, stream);
       break;
     case EPI_SWIGLU_BF16:
       FLITE_REQUIRE(p.W2 != nullptr, "gemm(swiglu): up weight missing");

@@ -9,6 +9,8 @@ enum GemmEpilogue {
   EPI_STORE_F32 = 1,    // out_f32[m][n]  = acc + bias[n]
   EPI_RESID_F32 = 2,    // out_f32[m][n] += gate[seg(m)][n] * (acc + bias[n])   (gated residual, model.py:289,297,301)
   EPI_SWIGLU_BF16 = 3,  // out_bf16[m][f] = silu(A.Wg[f]) * (A.Wu[f])            (LigerSwiGLUMLP gate/up)
+  EPI_QKV_NORM_BF16 = 5,  // out_bf16 = acc + bias; columns [0, norm_cols) (heads of 256) first get 2-D RoPE
+                          // (columns [0, rope_cols)) and QKNorm's per-head RMSNorm (model.py:166-180,197)
 };
 
 struct GemmParams {
@@ -38,6 +40,12 @@ struct GemmParams {
   float* sk_ws = nullptr;
   int* sk_flags = nullptr;
   int sk_tiles = 0;  // set by the launcher
+  // EPI_QKV_NORM_BF16: RoPE tables fp32 [rope_tokens, 128] (row m uses table row m % rope_tokens)
+  const float* rope_cos = nullptr;
+  const float* rope_sin = nullptr;
+  long rope_tokens = 0;
+  int rope_cols = 0, norm_cols = 0;
+  float norm_eps = 1e-6f;
   unsigned long long* sk_stamps = nullptr;  // diagnostic build only (FLITE_SK_STAMPS)
 };
 

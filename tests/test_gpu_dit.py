@@ -159,3 +159,37 @@ def test_forward_full_width(lh, lw):
     p = psnr(out, ref)
     print(f"full-width depth-1 10B-layout forward at {8 * lw}x{8 * lh}: PSNR {p:.2f} dB vs fp32 oracle")
     assert p >= 40.0
+
+
+def test_qk_norm_fusion_matches_separate_kernel(tmp_path):
+    """RoPE + QK-norm fused into the qkv / cross-q GEMM epilogue (gemm.hip EPI_QKV_NORM_BF16) vs the separate
+    rope_qknorm kernel (FLITE_NO_QK_FUSION=1, in a child process: the switch is read once per process). The
+    fused path skips one bf16 rounding of q/k, so the outputs agree to rounding, not bit for bit."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    script = tmp_path / "fwd.py"
+    script.write_text(
+        "import sys, torch\n"
+        f"sys.path[:0] = [{str(root / 'f-lite_amd')!r}, {str(root)!r}]\n"
+        "from f_lite import DiT\nfrom f_lite.model import PRESETS\n"
+        "cfg = dict(PRESETS['10b']); cfg['depth'] = 2\n"
+        "m = DiT.random(seed=0, device='cuda', **cfg)\n"
+        "g = torch.Generator().manual_seed(3)\n"
+        "x = torch.randn(2, 16, 64, 64, generator=g).bfloat16().cuda()\n"
+        "c = torch.randn(2, 512, 4096, generator=g).bfloat16().cuda()\n"
+        "t = torch.tensor([0.6, 0.6]).bfloat16().cuda()\n"
+        "torch.save(m(x, c, None, t, output_dtype=torch.float32).cpu(), sys.argv[1])\n")
+    outs = []
+    for i, extra in enumerate(({}, {"FLITE_NO_QK_FUSION": "1"})):
+        f = tmp_path / f"o{i}.pt"
+        r = subprocess.run([sys.executable, str(script), str(f)], env=dict(os.environ, **extra), capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(torch.load(f, weights_only=True))
+    p = psnr(outs[0], outs[1])
+    print(f"fused vs separate RoPE/QK-norm (10B layout, depth 2, 512^2): {p:.2f} dB")
+    assert p >= 45.0
