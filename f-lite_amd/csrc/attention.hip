@@ -123,19 +123,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
-// Diagnostic build only (f-lite_amd/tools/attn_probe.hip): per-workgroup s_memrealtime stamps into
-// p.stamps[blockIdx.x * 4 + i]: 0 start, 1 main loop done, 2 end, 3 XCC id << 32 | HW_ID.
-#ifdef FLITE_ATTN_STAMPS
-#define ATTN_STAMP(i)                                                                                  \
-  do {                                                                                                 \
-    if (tid == 0 && p.stamps) p.stamps[blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();       \
-  } while (0)
-#else
-#define ATTN_STAMP(i) \
-  do {                \
-  } while (0)
-#endif
-
 // BOUNDED: every score s*scale is known to lie in [-max_score, max_score] (QK-normed q and k: |q|,|k| <= 16
 // for head_dim 256, so |q.k|/16 <= 16 -- model.py:180,197 precede every attention call of the DiT). Softmax is
 // shift-invariant, so the running max is replaced by the fixed bound: no row max, no O/l rescale, p <= 1.
@@ -145,12 +132,6 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  ATTN_STAMP(0);
-#ifdef FLITE_ATTN_STAMPS
-  if (tid == 0 && p.stamps)
-    p.stamps[blockIdx.x * 4 + 3] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
-                                   (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
-#endif
   // Work decode. Phase A (blocks [0, nA)): one 128-row q-tile of one (sequence, head), all keys. Phase B
   // (the rest): key range `chunk` of the tail rows [n_main*QT, q_len) of one (sequence, head).
   // Each phase is remapped XCD-aware, so consecutive workgroups of one XCD share a (sequence, head) and its
@@ -267,68 +248,14 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) v_off[dt] = (dt ^ vq) * 64;
 
-  // BOUNDED: compute(buf, tn) also streams tile tn (tn < 0: none) into buffer buf ^ 1: the 8 K pieces in one
-  // burst at the start, the 8 V pieces one per MFMA pair over the first half of the S phase (an LDS-DMA costs
-  // ~60 issue cycles; an issue ~1 µs from the end-of-tile wait exposes its landing latency).
-  auto compute = [&](const int buf, const int tn) {
+  // Online-softmax tile step (unbounded scores only; the bounded path runs the pipelined loop below): S^T for both
+  // 32-key halves of LDS buffer buf, the running-max rescale, then O^T += V^T P^T.
+  auto compute = [&](const int buf) {
     const char* Kb = kbase + buf * TILE;
     const char* Vb = vbase + buf * TILE;
-    i32x4 krs_n = {0, 0, 0, 0}, vrs_n = {0, 0, 0, 0};
-    if (BOUNDED && tn >= 0) {
-      const long rows_left = k_len - (long)tn * KT;
-      krs_n = make_rsrc(p.k + k_base + (long)tn * KT * p.k_row_stride,
-                        (unsigned)min(rows_left * p.k_row_stride * 2, 0x7fffffffL));
-      vrs_n = make_rsrc(p.v + v_base + (long)tn * KT * p.v_row_stride,
-                        (unsigned)min(rows_left * p.v_row_stride * 2, 0x7fffffffL));
-    }
-    auto piece = [&](int i) {  // i < 8: K piece i, else V piece i - 8
-#ifdef FLITE_ATTN_ABL_NODMA
-      if (false) {
-#else
-      if (tn >= 0) {
-#endif
-        const unsigned dst = lds0 + (buf ^ 1) * TILE + (wave * 8 + (i & 7)) * 1024;
-        if (i < 8)
-          blds16(krs_n, k_src[i], dst + K_OFF);
-        else
-          blds16(vrs_n, v_src[i - 8], dst + V_OFF);
-      }
-    };
     f32x16 s0, s1;
-    if constexpr (BOUNDED) {
-      // S^T for both 32-key halves, two accumulation chains; K fragments 3 k-steps ahead of their MFMAs,
-      // order pinned by sched_barrier (the loop then holds ~24 K-fragment registers, not 128).
-      bf16x8 k0[16], k1[16];
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        k0[s] = *(const bf16x8*)(Kb + k_off[s]);
-        k1[s] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) piece(i);  // K of the next tile: needed first, issued first
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        if (s + 3 < 16) {
-          k0[s + 3] = *(const bf16x8*)(Kb + k_off[s + 3]);
-          k1[s + 3] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s + 3]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (s == 0) {
-          mfma_s_first(s0, k0[0], qf[0]);
-          mfma_s_first(s1, k1[0], qf[0]);
-        } else {
-          mfma_s(s0, k0[s], qf[s]);
-          mfma_s(s1, k1[s], qf[s]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (s < 8) piece(8 + s);  // V pieces in the first half of the S phase
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      mfma_read_fence(s0, s1);  // MFMA write of S -> VALU read (exp below)
-    } else {
-      // S^T for both 32-key halves: all 32 K fragments first, two independent accumulation chains
+    {
+      // all 32 K fragments first, two independent accumulation chains
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         s0[r] = 0.f;
@@ -354,7 +281,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
     }
-    if constexpr (!BOUNDED) {
+    {
       float tmax = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, fmaxf(s0[r], s1[r]));
@@ -374,18 +301,10 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       f32x16& sacc = kh ? s1 : s0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-#ifdef FLITE_ATTN_ABL_NOEXP
-        const float e = sacc[r];
-#else
         const float e = __builtin_amdgcn_exp2f(sacc[r] * sl2 - m_run);
-#endif
         sacc[r] = e;
         l_run += e;
       }
-#ifdef FLITE_ATTN_ABL_NOPV
-      asm volatile("" : "+v"(sacc));
-      continue;
-#endif
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 pk;
@@ -402,14 +321,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         for (int dt = 0; dt < 8; ++dt) {
           const s16x8 c = __builtin_shufflevector(lo[dt], hi[dt], 0, 1, 2, 3, 4, 5, 6, 7);
           const bf16x8 vf = __builtin_bit_cast(bf16x8, c);
-          if constexpr (BOUNDED) {  // O stays in AGPRs (no VALU ever touches it inside the loop)
-            if (dt == 0)
-              mfma_o<true>(o_acc[dt], vf, pk);
-            else
-              mfma_o<false>(o_acc[dt], vf, pk);
-          } else {  // the online rescale multiplies O by VALU every tile
-            o_acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pk, o_acc[dt], 0, 0, 0);
-          }
+          o_acc[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pk, o_acc[dt], 0, 0, 0);
         }
         // 16 transposed reads: 4 ahead, then one MFMA per two reads
         __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
@@ -423,18 +335,11 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     }
   };
 
-#ifdef FLITE_ATTN_ABL_NOBAR
-#define ATTN_TILE_SYNC() \
-  do {                   \
-  } while (0)
-#else
 #define ATTN_TILE_SYNC()                                \
   do {                                                  \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
     __syncthreads();                                    \
   } while (0)
-#endif
-#ifndef FLITE_ATTN_OLDLOOP
   if constexpr (BOUNDED) {
     // ---- software-pipelined key loop (bounded softmax) ----
     // Iteration j: phase A issues S_{j+1} = K_{j+1} . Q^T (K fragments from LDS) and, spread one per MFMA pair,
@@ -454,15 +359,8 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       const long rows_left = live ? k_len - (long)t * KT : 0;
       return make_rsrc(base + off + (long)t * KT * stride, (unsigned)max(0L, min(rows_left * stride * 2, 0x7fffffffL)));
     };
-#ifndef ATTN_KAHEAD
-#define ATTN_KAHEAD 3  // K fragment reads issued this many k-steps ahead of their MFMA pair
-#endif
-#ifndef ATTN_VAHEAD
-#define ATTN_VAHEAD 4  // V^T transposed reads issued this many MFMAs ahead
-#endif
-#ifndef ATTN_VDMA_B
-#define ATTN_VDMA_B 0  // 1: the V copies go in phase B (one per 4 MFMAs) instead of phase A
-#endif
+    constexpr int KAHEAD = 3;  // K fragment reads issued this many k-steps ahead of their MFMA pair
+    constexpr int VAHEAD = 4;  // V^T transposed reads issued this many MFMAs ahead
     f32x16 s0, s1;          // S of the tile whose softmax is pending
     u32x4 pa[4], pb[4];     // P^T operands (kh, 16-key half) of two consecutive tiles, bf16 pairs
     // phase A. KB: K buffer read by the S MFMAs; DKB / DVB: buffers the K / V copies land in; DMA: copies issued
@@ -477,16 +375,16 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       }
       bf16x8 k0[16], k1[16];
 #pragma unroll
-      for (int s = 0; s < ATTN_KAHEAD; ++s) {
+      for (int s = 0; s < KAHEAD; ++s) {
         k0[s] = *(const bf16x8*)(Kb + k_off[s]);
         k1[s] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s]);
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
-        if (s + ATTN_KAHEAD < 16) {
-          k0[s + ATTN_KAHEAD] = *(const bf16x8*)(Kb + k_off[s + ATTN_KAHEAD]);
-          k1[s + ATTN_KAHEAD] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s + ATTN_KAHEAD]);
+        if (s + KAHEAD < 16) {
+          k0[s + KAHEAD] = *(const bf16x8*)(Kb + k_off[s + KAHEAD]);
+          k1[s + KAHEAD] = *(const bf16x8*)(Kb + 32 * 512 + k_off[s + KAHEAD]);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (s == 0) {
@@ -497,16 +395,12 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
           mfma_s(s1, k1[s], qf[s]);
         }
         __builtin_amdgcn_sched_barrier(0);
-// FLITE_ATTN_ABL_*: diagnostic timing builds (wrong outputs). Prices on MI355X at T = 4096 (405 us): the DMA
-// copies 9 %, the V transposed reads 9 %, the softmax 0 % (hidden), the tile barrier 0 %.
-#ifdef FLITE_ATTN_ABL_NODMA
-        if constexpr (false) {
-#else
+// Round-1 ablation builds priced these at T = 4096 (405 us): the DMA copies 9 %, the V transposed reads 9 %,
+// the softmax 0 % (hidden), the tile barrier 0 %.
         if constexpr (DMA) {  // K pieces first (needed first), then V
-#endif
           if (s < 8)
             blds16(krs, k_src[s], lds0 + DKB * TILE + (wave * 8 + s) * 1024 + K_OFF);
-          else if (!ATTN_VDMA_B)
+          else
             blds16(vrs, v_src[s - 8], lds0 + DVB * TILE + (wave * 8 + s - 8) * 1024 + V_OFF);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -517,11 +411,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     auto softmax_elem = [&](u32x4 (&pn)[4], int e, float& e_prev) {
       const f32x16& sacc = e < 16 ? s0 : s1;
       const int r = e & 15;
-#ifdef FLITE_ATTN_ABL_NOEXP
-      const float v = sacc[r] * sl2 - m_run;
-#else
       const float v = __builtin_amdgcn_exp2f(sacc[r] * sl2 - m_run);
-#endif
       l_run += v;
       if (e & 1) {
         const bf16x2 pr = {(__bf16)e_prev, (__bf16)v};
@@ -530,30 +420,24 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       e_prev = v;
     };
     // phase B: O^T += V^T . P^T (operand pc) from Vbuf[VB]; EX: the softmax of the pending S into pn
-    auto phase_b = [&](auto vb_, auto ex_, u32x4 (&pc)[4], u32x4 (&pn)[4], int tv, bool v_live) {
+    auto phase_b = [&](auto vb_, auto ex_, u32x4 (&pc)[4], u32x4 (&pn)[4]) {
       constexpr int VB = decltype(vb_)::value;
       constexpr bool EX = decltype(ex_)::value;
       const char* Vb = vbase + VB * TILE;
-      const i32x4 vrs = ATTN_VDMA_B ? rsrc_tile(p.v, v_base, p.v_row_stride, tv, v_live) : i32x4{0, 0, 0, 0};
       float e_prev = 0.f;
       // MFMA m = 8 g + dt, g = (kh, s): V^T fragment from rows kh*32 + 16 s (+8), d-tile dt; reads 2 MFMAs ahead
       s16x4 lo[32], hi[32];
       auto rd = [&](int m) {
         const int g = m >> 3, dt = m & 7, kh = g >> 1, s = g & 1;
-#ifdef FLITE_ATTN_ABL_NOTR
-        lo[m] = s16x4{(short)kh, (short)s, (short)dt, 1};
-        hi[m] = lo[m];
-#else
         lo[m] = ds_tr16(Vb + (kh * 32 + 16 * s) * 512 + v_off[dt]);
         hi[m] = ds_tr16(Vb + (kh * 32 + 16 * s + 8) * 512 + v_off[dt]);
-#endif
       };
 #pragma unroll
-      for (int m = 0; m < ATTN_VAHEAD; ++m) rd(m);
+      for (int m = 0; m < VAHEAD; ++m) rd(m);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int m = 0; m < 32; ++m) {
-        if (m + ATTN_VAHEAD < 32) rd(m + ATTN_VAHEAD);
+        if (m + VAHEAD < 32) rd(m + VAHEAD);
         __builtin_amdgcn_sched_barrier(0);
         const int g = m >> 3, dt = m & 7;
         const s16x8 c = __builtin_shufflevector(lo[m], hi[m], 0, 1, 2, 3, 4, 5, 6, 7);
@@ -565,9 +449,6 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
           mfma_o<false>(o_acc[dt], vf, pk);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (EX) softmax_elem(pn, m, e_prev);
-        __builtin_amdgcn_sched_barrier(0);
-        if (ATTN_VDMA_B && (m & 3) == 1)
-          blds16(vrs, v_src[m >> 2], lds0 + (VB ^ 1) * TILE + (wave * 8 + (m >> 2)) * 1024 + V_OFF);
         __builtin_amdgcn_sched_barrier(0);
       }
     };
@@ -582,9 +463,9 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
           phase_a(I0{}, I1{}, I0{}, BT{}, t_begin + j + 2, j + 2 < nt, t_begin + j + 1, true);
       }
       if constexpr (P == 0)
-        phase_b(I0{}, hs_, pa, pb, t_begin + j + 1, j + 1 < nt);
+        phase_b(I0{}, hs_, pa, pb);
       else
-        phase_b(I1{}, hs_, pb, pa, t_begin + j + 1, j + 1 < nt);
+        phase_b(I1{}, hs_, pb, pa);
       ATTN_TILE_SYNC();
     };
     if (nt > 0) {
@@ -616,38 +497,26 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         iter(I0{}, BF{}, j);
       }
     }
-  } else
-#endif
-  if (nt > 0) {
+  } else if (nt > 0) {
     stage(t_begin, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // two tiles per iteration (static LDS buffer index), one exit; an odd last tile is peeled
     int j = 0;
     for (; j + 1 < nt; j += 2) {
-      if constexpr (BOUNDED) {
-        compute(0, t_begin + j + 1);
-      } else {
-        stage(t_begin + j + 1, 1);
-        compute(0, -1);
-      }
+      stage(t_begin + j + 1, 1);
+      compute(0);
       ATTN_TILE_SYNC();
-      const int t2 = j + 2 < nt ? t_begin + j + 2 : -1;
-      if constexpr (BOUNDED) {
-        compute(1, t2);
-      } else {
-        if (t2 >= 0) stage(t2, 0);
-        compute(1, -1);
-      }
+      if (j + 2 < nt) stage(t_begin + j + 2, 0);
+      compute(1);
       ATTN_TILE_SYNC();
     }
     if (j < nt) {
-      compute(0, -1);
+      compute(0);
       ATTN_TILE_SYNC();
     }
   }
 
-  ATTN_STAMP(1);
   if constexpr (BOUNDED) o_acc_fence(o_acc);
   // keys past the end were staged as zero rows: each contributed exp2(0*sl2 - m) to l and 0 to O
   l_run += __shfl_xor(l_run, 32, 64);  // the two lane halves hold the sums of complementary keys
@@ -681,7 +550,6 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       if (tid == 0) *flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       if (*flag != p.n_split - 1) {  // not the last arriver (uniform)
-        ATTN_STAMP(2);
         return;
       }
       if (tid == 0) {
@@ -728,7 +596,6 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         st.y = pack2bf(acc[2] * inv, acc[3] * inv);
         *(u32x2*)(p.o + (long)(q_start + row) * p.o_row_stride + (long)h * p.o_head_stride + d) = st;
       }
-      ATTN_STAMP(2);
       return;
     }
   }
@@ -754,7 +621,6 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       *(u32x4*)(orow + i * 32 + 16 * rp + 8 * hh) = w;
     }
   }
-  ATTN_STAMP(2);
 }
 
 bool attr_done = false;

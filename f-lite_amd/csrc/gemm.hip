@@ -16,6 +16,7 @@
 // the per-lane SOURCE offset and undone on the ds_read), two LDS buffers, one barrier per 64-deep k-tile.
 // Fragments are register double-buffered at half-k-step granularity (W: two sets of 4; A: low/high halves of
 // 8), so every ds_read overlaps MFMAs of the previous half-step, including across the k-tile barrier.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -272,17 +273,10 @@ struct GemmCta {
     for (int i = 0; i < 4; ++i) ah[i] = rd_a<BUF>(1, 4 + i);
     mfma_half(acc, wy, al, 0);
     interleave<4>();
-// GEMM_ABL_*: diagnostic timing builds only (wrong results). On MI355X the DMA wait costs 3.5 % of the gate/up
-// GEMM and 8-11 % of the K = 12288 projections (operands streamed from HBM), nothing at K = 3072, N <= 9216.
-#if defined(GEMM_ABL_NOVMWAIT)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#elif defined(GEMM_ABL_NOSYNC)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
+    // Round-1 ablation builds priced this wait on MI355X: 3.5 % of the gate/up GEMM and 8-11 % of the K = 12288
+    // projections (operands streamed from HBM), nothing at K = 3072, N <= 9216.
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-#endif
     // The two waves of a SIMD (w, w + 4) issue their copies of tile t+2 a half-step apart, so one of them
     // keeps the MFMA pipe fed while the other spends issue cycles on LDS-DMA. Not in CONV mode: there the
     // per-tap gather addressing makes the split schedule 1.9x slower (tools/kbench_conv.py).
@@ -583,12 +577,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-// linear tile id -> (m0, n0): groups of GEMM_GROUP M-tiles, M-fastest inside a group (L2 reuse of W columns)
+// linear tile id -> (m0, n0): groups of 6 M-tiles, M-fastest inside a group (L2 reuse of W columns)
 __device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0, int& n0, int bm = BM) {
-#ifndef GEMM_GROUP
-#define GEMM_GROUP 6  // kbench_gemm A/B on MI355X: 4-6 beat 8 by 1.5-2.5 % (gate/up, 8192^3), 2 and 16 lose
-#endif
-  constexpr int GROUP = GEMM_GROUP;
+  constexpr int GROUP = 6;  // kbench_gemm A/B on MI355X: 4-6 beat 8 by 1.5-2.5 % (gate/up, 8192^3), 2 and 16 lose
   const int group_size = GROUP * num_n;
   const int gid = L / group_size;
   const int first_m = gid * GROUP;
@@ -599,19 +590,6 @@ __device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0
 }
 
 __device__ __forceinline__ long sk_start(int g, long I, int G) { return (long)g * I / G; }
-
-// Diagnostic build only (f-lite_amd/tools/sk_probe.hip): per-workgroup s_memrealtime stamps of the stream-K
-// phases into p.sk_stamps[wg * 8 + i].
-#ifdef FLITE_SK_STAMPS
-#define SK_STAMP(i)                                                                                   \
-  do {                                                                                                \
-    if (c.tid == 0 && p.sk_stamps) p.sk_stamps[wg * 8 + (i)] = __builtin_amdgcn_s_memrealtime();     \
-  } while (0)
-#else
-#define SK_STAMP(i) \
-  do {              \
-  } while (0)
-#endif
 
 // Stream-K + data-parallel (persistent grid G = one workgroup per CU). Tiles [0, sk_tiles) are cut into
 // G contiguous, equal ranges of k-tile iterations (I / G < nk, so a range touches at most 2 tiles); the
@@ -626,14 +604,14 @@ __device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&ac
   const GemmParams& p = c.p;
   int m0, n0;
   const int G = gridDim.x;
+  const int Gs = p.sk_wgs;  // workgroups [0, Gs) share the stream-K iterations
   const int T = num_m * num_n;
   const long I = (long)p.sk_tiles * nk;
-  const long it0 = sk_start(wg, I, G), it1 = sk_start(wg + 1, I, G);
+  const long it0 = wg < Gs ? sk_start(wg, I, Gs) : I, it1 = wg < Gs ? sk_start(wg + 1, I, Gs) : I;
   const int jf = (int)(it0 / nk);            // tile of the first segment
   const int jl = (int)((it1 - 1) / nk);      // tile of the last segment
   const bool has_range = it1 > it0;
   f32x4* slab = (f32x4*)p.sk_ws;
-  SK_STAMP(0);
 
   // (1) data-parallel tiles: every workgroup in step, so the XCD-local tile block shares A/W k-slices in L2
   for (int L = p.sk_tiles + wg; L < T; L += G) {
@@ -642,7 +620,6 @@ __device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&ac
     c.mainloop(acc, 0, nk);
     c.epilogue(acc, m0, n0);
   }
-  SK_STAMP(1);
   // (2) partial: the last segment when it does not reach its tile's end
   if (has_range) {
     const long t0 = (long)jl * nk;
@@ -666,7 +643,6 @@ __device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&ac
       if (c.tid == 0) __hip_atomic_store(p.sk_flags + wg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  SK_STAMP(2);
   // (3) finisher: the first segment when it reaches its tile's end
   if (has_range) {
     const long t0 = (long)jf * nk;
@@ -675,14 +651,13 @@ __device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&ac
       tile_origin(jf, num_m, num_n, m0, n0);
       c.setup_tile(m0, n0);
       c.mainloop(acc, kb, kend);
-      SK_STAMP(3);
       if (kb > 0) {
         // producers: workgroups h < wg whose range ends inside this tile
         int h_lo = wg;
-        while (h_lo > 0 && sk_start(h_lo, I, G) > t0) --h_lo;
+        while (h_lo > 0 && sk_start(h_lo, I, Gs) > t0) --h_lo;
         if (c.tid == 0) {
           for (int h = h_lo; h < wg; ++h) {
-            if (sk_start(h + 1, I, G) == sk_start(h, I, G)) continue;  // empty range: no partial
+            if (sk_start(h + 1, I, Gs) == sk_start(h, I, Gs)) continue;  // empty range: no partial
             long spins = 0;
             while (__hip_atomic_load(p.sk_flags + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
               __builtin_amdgcn_s_sleep(2);
@@ -692,10 +667,9 @@ __device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&ac
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        SK_STAMP(4);
         __syncthreads();
         for (int h = h_lo; h < wg; ++h) {
-          if (sk_start(h + 1, I, G) == sk_start(h, I, G)) continue;
+          if (sk_start(h + 1, I, Gs) == sk_start(h, I, Gs)) continue;
           const f32x4* src = slab + (size_t)h * (BM * BN / 4);
 #pragma unroll
           for (int mi = 0; mi < 8; ++mi)
@@ -709,13 +683,6 @@ __device__ __forceinline__ void stream_k_body(GemmCta<EPI, false>& c, f32x4 (&ac
       c.epilogue(acc, m0, n0);
     }
   }
-  SK_STAMP(5);
-#ifdef FLITE_SK_STAMPS
-  if (c.tid == 0 && p.sk_stamps) {
-    p.sk_stamps[wg * 8 + 6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-    p.sk_stamps[wg * 8 + 7] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-  }
-#endif
 }
 
 // One launch: data-parallel (grid = tiles, one output tile per workgroup) or, when the launcher set
@@ -747,23 +714,33 @@ int g_num_cu = 0;
 
 // Stream-K split for a workspace-carrying launch, in units of one k-tile iteration of one workgroup:
 //   data parallel  ceil(T / G) * nk
-//   stream-K       floor(T / G) * nk + 1.1 * (T % G) * nk / G + 24
-// The 1.1 and 24 (partial-slab write/read, two extra pipeline prologues, finisher epilogue) are fitted to
-// tools/sk_probe.py timelines on MI355X: at M = 8224, N = 3072 stream-K wins at K = 12288 (-11 %) and loses
-// at K = 3072 (+6 %), so it is taken only with a 3 % margin.
-int choose_sk_tiles(const GemmParams& p, int T) {
+//   stream-K       floor(T / G) * nk + 1.1 * rem * nk / Gs + 24 + 5.5 * (ceil(Gs / rem) - 1)
+// over Gs workgroups sharing the rem = T % G leftover tiles. The 1.1 and 24 (partial-slab write/read, two extra
+// pipeline prologues, finisher epilogue) are fitted to round-1 timelines on MI355X (M = 8224, N = 3072:
+// stream-K wins at K = 12288 (-11 %), loses at K = 3072 (+6 %)); 5.5 per extra partial a finisher adds is
+// fitted to M = 16448, N = 3072 (12 leftover tiles cut 22 ways cost +230 us over the first two terms).
+// Returns the tile count and sets *gs; taken only with a 3 % margin.
+int choose_sk_tiles(const GemmParams& p, int T, int* gs) {
+  *gs = 0;
   if (p.sk_ws == nullptr || p.sk_flags == nullptr || g_num_cu <= 0) return 0;
   const int G = g_num_cu;
   const int rem = T % G;
   if (rem == 0) return 0;
   const double nk = p.K / BK;
-  if (rem * nk < 2.0 * G) return 0;  // ranges of at least 2 k-tiles
-#ifdef FLITE_SK_STAMPS
-  if (getenv("FLITE_SK_FORCE") != nullptr) return rem;  // diagnostic build: time the split where it is not taken
-#endif
   const double dp = (double)(T / G + 1) * nk;
-  const double sk = (double)(T / G) * nk + 1.1 * rem * nk / G + 24.0;
-  return sk < 0.97 * dp ? rem : 0;
+  double best = 0.97 * dp;
+  for (int f = 2;; ++f) {  // Gs = f * rem: each leftover tile cut into about f ranges
+    const int Gs = std::min(G, f * rem);
+    if (rem * nk < 2.0 * Gs) break;  // ranges of at least 2 k-tiles
+    const int fan = (Gs + rem - 1) / rem;
+    const double sk = (double)(T / G) * nk + 1.1 * rem * nk / Gs + 24.0 + 5.5 * (fan - 1);
+    if (sk < best) {
+      best = sk;
+      *gs = Gs;
+    }
+    if (Gs == G) break;
+  }
+  return *gs ? rem : 0;
 }
 
 // Tile height: 224-row tiles (MI = 7) where they take fewer rounds x tile size than 256-row tiles on the
@@ -782,7 +759,7 @@ template <int EPI>
 int launch(GemmParams p, hipStream_t s) {
   const int num_n = (p.N + BN - 1) / BN;
   const int T = (p.M + BM - 1) / BM * num_n;
-  p.sk_tiles = choose_sk_tiles(p, T);
+  p.sk_tiles = choose_sk_tiles(p, T, &p.sk_wgs);
   if (p.conv_in != nullptr) {
     hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true, 8>), dim3(T), dim3(NT), LDS_BYTES, s, p);
   } else if (p.sk_tiles) {

@@ -40,13 +40,13 @@ struct GemmParams {
   float* sk_ws = nullptr;
   int* sk_flags = nullptr;
   int sk_tiles = 0;  // set by the launcher
+  int sk_wgs = 0;    // set by the launcher: workgroups sharing the stream-K iterations
   // EPI_QKV_NORM_BF16: RoPE tables fp32 [rope_tokens, 128] (row m uses table row m % rope_tokens)
   const float* rope_cos = nullptr;
   const float* rope_sin = nullptr;
   long rope_tokens = 0;
   int rope_cols = 0, norm_cols = 0;
   float norm_eps = 1e-6f;
-  unsigned long long* sk_stamps = nullptr;  // diagnostic build only (FLITE_SK_STAMPS)
 };
 
 // bytes of the stream-K workspace (partials + flags) for the current device
@@ -77,7 +77,6 @@ struct AttnParams {
   void* split_ws = nullptr;
   long split_ws_bytes = 0;
   int n_main = 0, n_split = 0;  // set by the launcher
-  unsigned long long* stamps = nullptr;  // diagnostic build only (FLITE_ATTN_STAMPS)
 };
 
 int attn_fwd(const AttnParams& p, hipStream_t stream);

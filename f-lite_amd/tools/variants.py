@@ -1,0 +1,122 @@
+"""A/B builds of one kernel source with compile-time knobs (diagnostic; not part of the product library).
+
+build (CPU container):  python tools/variants.py build gemm NAME -DKNOB=1 ...
+    compiles csrc/<src>.hip with the knobs and links it with the product objects of every other source into
+    tools/variants/NAME/libflite_hip.so (git-ignored).
+run (GPU box):          python tools/variants.py run gemm NAME1 NAME2 ... [--rounds R]
+    times the DiT GEMM (or attention) shapes under each variant, alternating variants per round, one
+    subprocess per (variant, round) with FLITE_LIB pointing at the variant library.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+PKG = HERE.parent
+sys.path.insert(0, str(PKG))
+
+GEMM_SHAPES = [  # name, M, N, K, epilogue
+    ("gateup", 8224, 24576, 3072, "swiglu"),
+    ("qkv", 8224, 9216, 3072, "store"),
+    ("cross_q", 8224, 3072, 3072, "store"),
+    ("proj", 8224, 3072, 3072, "resid"),
+    ("down", 8224, 3072, 12288, "resid"),
+]
+
+
+def build(src, name, defines):
+    import build_native as bn
+
+    bn.build(verbose=False)
+    out = HERE / "variants" / name
+    out.mkdir(parents=True, exist_ok=True)
+    obj = out / f"{src}.o"
+    cmd = [bn.HIPCC, *bn.CFLAGS, *defines, "-c", str(bn.CSRC / f"{src}.hip"), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr[-4000:])
+    objs = [str(obj)] + [str(bn.BUILD / (p.stem + ".o")) for p in bn._sources() if p.stem != src]
+    subprocess.run([bn.HIPCC, f"--offload-arch={bn.ARCH}", "-shared", "-fPIC", "-o", str(out / "libflite_hip.so"),
+                    *objs], check=True)
+    (out / "defines.json").write_text(json.dumps(defines))
+    print(f"built variant {name}: {defines}")
+
+
+def time_gemms(iters=20):
+    import torch
+    from f_lite import _native as nat
+
+    torch.manual_seed(0)
+    ws = nat.gemm_workspace("cuda")
+    res = {}
+    for name, M, N, K, epi in GEMM_SHAPES:
+        a = torch.randn(M, K, device="cuda").bfloat16()
+        if epi == "swiglu":
+            w = (torch.randn(N // 2, K, device="cuda") * 0.05).bfloat16()
+            w2 = (torch.randn(N // 2, K, device="cuda") * 0.05).bfloat16()
+            out = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
+            kw = dict(epilogue=nat.EPI_SWIGLU_BF16, w2=w2)
+        elif epi == "resid":
+            w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+            out = torch.zeros(M, N, device="cuda")
+            kw = dict(epilogue=nat.EPI_RESID_F32, gate=torch.randn(2, N, device="cuda"), gate_seg_stride=N,
+                      rows_per_seg=M // 2)
+        else:
+            w = (torch.randn(N, K, device="cuda") * 0.05).bfloat16()
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            kw = dict(epilogue=nat.EPI_STORE_BF16)
+        for _ in range(3):
+            nat.gemm(a, w, out=out, workspace=ws, **kw)
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(iters):
+            nat.gemm(a, w, out=out, workspace=ws, **kw)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+        res[name] = (ms, 2.0 * M * N * K / ms / 1e9)
+    return res
+
+
+def main():
+    mode, src = sys.argv[1], sys.argv[2]
+    if mode == "build":
+        build(src, sys.argv[3], sys.argv[4:])
+        return
+    if mode == "child":
+        print("RESULT " + json.dumps(time_gemms()), flush=True)
+        return
+    args = sys.argv[3:]
+    rounds = 3
+    if "--rounds" in args:
+        i = args.index("--rounds")
+        rounds = int(args[i + 1])
+        del args[i:i + 2]
+    names = args
+    table = {n: [] for n in names}
+    for r in range(rounds):
+        for n in names:
+            lib = HERE / "variants" / n / "libflite_hip.so"
+            env = dict(os.environ, FLITE_LIB=str(lib))
+            p = subprocess.run([sys.executable, __file__, "child", src], env=env, capture_output=True, text=True,
+                               timeout=300)
+            line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
+            if p.returncode != 0 or not line:
+                print(p.stdout[-2000:], p.stderr[-2000:])
+                sys.exit(1)
+            table[n].append(json.loads(line[0][7:]))
+            print(f"round {r} {n}: " + " ".join(f"{k} {v[0]*1e3:.1f}us/{v[1]:.0f}TF" for k, v in table[n][-1].items()),
+                  flush=True)
+    print("== median us per shape")
+    for n in names:
+        shapes = table[n][0].keys()
+        med = {k: sorted(t[k][0] for t in table[n])[len(table[n]) // 2] * 1e3 for k in shapes}
+        print(n, " ".join(f"{k} {v:.1f}" for k, v in med.items()), f"sum {sum(med.values()):.1f}")
+
+
+if __name__ == "__main__":
+    main()
