@@ -7,6 +7,7 @@
 #include "kernels.h"
 #include "dit.h"
 #include "fp8.h"
+#include "t5.h"
 #include <math.h>
 
 namespace flite {
@@ -231,6 +232,32 @@ int flite_dit_set_timesteps(flite_dit* dit, void* stream, const float* t, int n,
 
 int flite_gather_rows(void* stream, const void* src, void* dst, const int* idx, long n, int cols) {
   return gather_rows((const bf16_t*)src, (bf16_t*)dst, idx, n, cols, (hipStream_t)stream);
+}
+
+int flite_t5_attention(void* stream, const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                       void* o, long ldo, const int* bucket, const void* rel_weight, const float* mask, int B,
+                       int L, int H) {
+  T5AttnParams p;
+  p.q = (const bf16_t*)q;
+  p.k = (const bf16_t*)k;
+  p.v = (const bf16_t*)v;
+  p.o = (bf16_t*)o;
+  p.ldq = ldq;
+  p.ldk = ldk;
+  p.ldv = ldv;
+  p.ldo = ldo;
+  p.bucket = bucket;
+  p.rel_weight = (const bf16_t*)rel_weight;
+  p.mask = mask;
+  p.B = B;
+  p.L = L;
+  p.H = H;
+  return t5_attention(p, (hipStream_t)stream);
+}
+
+int flite_embed_rows_f32(void* stream, const void* table, const int* ids, float* out, long n, int cols, long vocab) {
+  FLITE_REQUIRE(table && ids && out, "flite_embed_rows_f32: null argument");
+  return embed_rows_f32((const bf16_t*)table, ids, out, n, cols, vocab, (hipStream_t)stream);
 }
 
 int flite_cfg_euler(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,

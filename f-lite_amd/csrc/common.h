@@ -38,6 +38,14 @@ __device__ __forceinline__ float silu_f(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
 }
 
+// GELU, tanh approximation (transformers' "gelu_new", the T5 v1.1 gated FF): 0.5 x (1 + tanh(u)),
+// u = sqrt(2/pi) (x + 0.044715 x^3), with tanh(u) = 1 - 2 / (1 + e^{2u}).
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(2.8853900817779268f * u));
+  return 0.5f * x * (1.0f + t);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -112,6 +112,7 @@ constexpr int SG_MFMA = 0x008, SG_DSR = 0x100;
 // tiles where 256 rows leave a last wave of tiles mostly empty; the A staging still copies 256 rows).
 template <int EPI, bool CONV, int MI = 8>
 struct GemmCta {
+  static constexpr bool GATED_FF = EPI == EPI_SWIGLU_BF16 || EPI == EPI_GEGLU_BF16;  // W = gate | W2 = up, N = 2F
   static constexpr int WM = MI * 16;  // output rows per wave_m
   static constexpr int BMV = 2 * WM;  // output rows per tile
   const GemmParams& p;
@@ -135,8 +136,8 @@ struct GemmCta {
     lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr_of(smem));
     a_rsrc = CONV ? make_rsrc(p.conv_in, (unsigned)p.conv_in_bytes) : make_rsrc(p.A, (unsigned)((long)p.M * p.lda * 2));
     // SwiGLU: W rows 8w + 64i lie in 16-row sub-tile (w>>1) + 4i, whose parity (gate / up) is (w>>1)&1
-    const bf16_t* wsrc = (EPI == EPI_SWIGLU_BF16 && ((wave >> 1) & 1)) ? p.W2 : p.W;
-    const long w_rows = EPI == EPI_SWIGLU_BF16 ? (long)(p.N >> 1) : (long)p.N;
+    const bf16_t* wsrc = (GATED_FF && ((wave >> 1) & 1)) ? p.W2 : p.W;
+    const long w_rows = GATED_FF ? (long)(p.N >> 1) : (long)p.N;
     w_rsrc = make_rsrc(wsrc, (unsigned)(w_rows * p.ldw * 2));
     // Fragment reads (16x16x32 operand map): lane l holds row (l & 15), k = 8*(l>>4) + 0..7 of the 32-deep
     // k-step s -> 16-B chunk 4s + (l>>4) of a 128-B tile row. Rows: W tile wave_n*64 + ni*16 + (l&15),
@@ -177,7 +178,7 @@ struct GemmCta {
         const int chunk = (lane & 7) ^ swz(row);
         const int wn = min(n0 + row, p.N - 1);
         long wrow = wn;
-        if constexpr (EPI == EPI_SWIGLU_BF16) {
+        if constexpr (GATED_FF) {
           // virtual row wn: sub-tile wn>>4 is gate (even) / up (odd) of output columns (wn>>5)*16 + (wn&15)
           wrow = (long)(wn >> 5) * 16 + (wn & 15);
         }
@@ -489,7 +490,7 @@ struct GemmCta {
     if constexpr (EPI == EPI_QKV_NORM_BF16) {
       qkv_norm_epilogue(acc, m0, n0, m_base, n_base);
       return;
-    } else if constexpr (EPI == EPI_SWIGLU_BF16) {
+    } else if constexpr (GATED_FF) {
       // pairs (ni=0 gate, ni=1 up), (ni=2 gate, ni=3 up) -> output column (n0/2 + wave_n*32 + pair*16 + 4*(lane>>4))
       const int F = p.N >> 1;
 #pragma unroll
@@ -504,8 +505,13 @@ struct GemmCta {
           const f32x4 g = acc[mi][2 * pr];
           const f32x4 u = acc[mi][2 * pr + 1];
           u32x2 v;
-          v.x = pack2bf(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
-          v.y = pack2bf(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
+          if constexpr (EPI == EPI_SWIGLU_BF16) {
+            v.x = pack2bf(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
+            v.y = pack2bf(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
+          } else {
+            v.x = pack2bf(gelu_tanh_f(g[0]) * u[0], gelu_tanh_f(g[1]) * u[1]);
+            v.y = pack2bf(gelu_tanh_f(g[2]) * u[2], gelu_tanh_f(g[3]) * u[3]);
+          }
           *(u32x2*)(orow + oc) = v;
         }
       }
@@ -795,6 +801,7 @@ int gemm_init() {
   FLITE_HIP_CHECK(set_attrs<EPI_STORE_F32>());
   FLITE_HIP_CHECK(set_attrs<EPI_RESID_F32>());
   FLITE_HIP_CHECK(set_attrs<EPI_SWIGLU_BF16>());
+  FLITE_HIP_CHECK(set_attrs<EPI_GEGLU_BF16>());
   FLITE_HIP_CHECK(set_attrs<EPI_QKV_NORM_BF16>());
   {
     int dev = 0;
@@ -869,6 +876,12 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
       FLITE_REQUIRE(p.N % 32 == 0, "gemm(swiglu): F must be a multiple of 16");
       FLITE_REQUIRE(p.bias == nullptr, "gemm(swiglu): bias not supported");
       launch<EPI_SWIGLU_BF16>(p, stream);
+      break;
+    case EPI_GEGLU_BF16:
+      FLITE_REQUIRE(p.W2 != nullptr, "gemm(geglu): wi_1 weight missing");
+      FLITE_REQUIRE(p.N % 32 == 0, "gemm(geglu): F must be a multiple of 16");
+      FLITE_REQUIRE(p.bias == nullptr, "gemm(geglu): bias not supported");
+      launch<EPI_GEGLU_BF16>(p, stream);
       break;
     default:
       FLITE_REQUIRE(false, "gemm: unknown epilogue");

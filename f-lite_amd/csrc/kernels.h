@@ -9,6 +9,7 @@ enum GemmEpilogue {
   EPI_STORE_F32 = 1,    // out_f32[m][n]  = acc + bias[n]
   EPI_RESID_F32 = 2,    // out_f32[m][n] += gate[seg(m)][n] * (acc + bias[n])   (gated residual, model.py:289,297,301)
   EPI_SWIGLU_BF16 = 3,  // out_bf16[m][f] = silu(A.Wg[f]) * (A.Wu[f])            (LigerSwiGLUMLP gate/up)
+  EPI_GEGLU_BF16 = 6,   // out_bf16[m][f] = gelu_tanh(A.Wg[f]) * (A.Wu[f])     (T5 DenseGatedActDense wi_0 / wi_1)
   EPI_QKV_NORM_BF16 = 5,  // out_bf16 = acc + bias; columns [0, norm_cols) (heads of 256) first get 2-D RoPE
                           // (columns [0, rope_cols)) and QKNorm's per-head RMSNorm (model.py:166-180,197)
 };

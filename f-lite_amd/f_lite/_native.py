@@ -18,6 +18,7 @@ EPI_STORE_BF16 = 0
 EPI_STORE_F32 = 1
 EPI_RESID_F32 = 2
 EPI_SWIGLU_BF16 = 3
+EPI_GEGLU_BF16 = 6
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
@@ -62,6 +63,8 @@ SIGNATURES = {
     "flite_rmsnorm_modulate": (_i, [_vp, _vp, _i, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_rope_qknorm": (_i, [_vp, _vp, _l, _l, _i, _i, _vp, _vp, _l, _f]),
     "flite_gather_rows": (_i, [_vp, _vp, _vp, _vp, _l, _i]),
+    "flite_t5_attention": (_i, [_vp, _vp, _l, _vp, _l, _vp, _l, _vp, _l, _vp, _vp, _vp, _i, _i, _i]),
+    "flite_embed_rows_f32": (_i, [_vp, _vp, _vp, _vp, _l, _i, _l]),
     "flite_rope_tables": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _i]),
     "flite_timestep_embedding": (_i, [_vp, _vp, _vp, _i, _i, _i]),
     "flite_init_param": (_i, [_vp, _vp, _i, _l, _cp, _ull, _d, _i]),
@@ -176,9 +179,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, *, out=None, epilogue=EPI_
     N = w.shape[0]
     if a.stride(1) != 1 or w.stride(1) != 1:
         raise FliteError("gemm: operands must be K-contiguous")
-    if epilogue == EPI_SWIGLU_BF16:
+    if epilogue in (EPI_SWIGLU_BF16, EPI_GEGLU_BF16):
         if w2 is None or w2.shape != w.shape:
-            raise FliteError("gemm(swiglu): w2 must match w")
+            raise FliteError("gemm(swiglu/geglu): w2 must match w")
         Nv = 2 * N
         if out is None:
             out = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)

@@ -87,6 +87,33 @@ def resolve_embeds(pipe: FLitePipeline, prompt: str, negative_prompt: Optional[s
     return pos, neg, "SYNTHETIC prompt embeddings (hash of the prompt text; no text encoder on this path)"
 
 
+def attach_text_encoder(pipe: FLitePipeline, spec: str, tokenizer: Optional[str], device):
+    """--text_encoder random:<t5 preset> (seeded synthetic T5 weights) or a local T5 folder (config.json +
+    model*.safetensors); --tokenizer a local tokenizer folder (transformers AutoTokenizer, offline), else the
+    byte-level SyntheticTokenizer."""
+    from .text_encoder import T5_PRESETS, SyntheticTokenizer, T5Encoder
+
+    if spec.startswith("random:"):
+        preset = spec.split(":", 1)[1]
+        if preset not in T5_PRESETS:
+            raise ValueError(f"unknown T5 preset {preset!r}; one of {sorted(T5_PRESETS)}")
+        enc = T5Encoder.random(seed=0, device=device, **T5_PRESETS[preset])
+    else:
+        enc = T5Encoder.from_pretrained(spec, device=device)
+    if enc.config.d_model != pipe.dit_model.config.cross_attn_input_size:
+        raise ValueError(f"text encoder width {enc.config.d_model} != DiT cross_attn_input_size "
+                         f"{pipe.dit_model.config.cross_attn_input_size}")
+    if tokenizer is not None:
+        from transformers import AutoTokenizer
+
+        tok = AutoTokenizer.from_pretrained(tokenizer, local_files_only=True)
+    else:
+        tok = SyntheticTokenizer(vocab_size=enc.config.vocab_size)
+        print("Tokenizer: SYNTHETIC byte-level ids (no tokenizer files given)")
+    pipe.text_encoder = enc
+    pipe.processor = tok
+
+
 def generate_images(
     prompt: str,
     output_file: str,
@@ -101,6 +128,8 @@ def generate_images(
     device: Optional[str] = None,
     num_images: int = 1,
     prompt_embeds: Optional[str] = None,
+    text_encoder: Optional[str] = None,
+    tokenizer: Optional[str] = None,
 ):
     """Generate images with the F-Lite pipeline (generate.py:13-113). Returns the written paths."""
     from . import _native
@@ -115,6 +144,8 @@ def generate_images(
     print(f"Using device: {device}")
     print(f"Loading model: {model}")
     pipe = load_pipeline(model, torch_device)
+    if text_encoder is not None:
+        attach_text_encoder(pipe, text_encoder, tokenizer, torch_device)
     if cpu_offload:
         pipe.enable_model_cpu_offload()  # no-op: weights stay resident in HBM
     if pipe.vae is not None:  # generate.py:77-78
@@ -164,6 +195,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--num_images", type=int, default=1)
     ap.add_argument("--prompt_embeds", default=None, help="safetensors with prompt_embeds [P, L, C] "
                     "(+ negative_prompt_embeds); default: synthetic embeddings")
+    ap.add_argument("--text_encoder", default=None, help="native T5 text encoder: random:<preset> "
+                    "(t5-xxl, tiny) or a local T5 folder; prompts are then encoded (pipeline.py:126-175)")
+    ap.add_argument("--tokenizer", default=None, help="local tokenizer folder for --text_encoder "
+                    "(default: byte-level synthetic ids)")
     return ap
 
 

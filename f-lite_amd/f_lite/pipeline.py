@@ -11,8 +11,10 @@ Differences by design:
     computed once per call;
   * the Euler accumulator, the residual stream and the modulate/gate/CFG math are fp32 (the reference
     rounds each to bf16; SURVEY §8d shows this is what lifts parity above the reference's own bf16 floor);
-  * text encoding is out of scope for this path: pass `prompt_embeds` (synthetic T5/Qwen hidden states);
-    a `text_encoder` with the reference's encode_prompt contract is still honoured if one is supplied.
+  * text encoding (pipeline.py:126-175) runs natively when the text encoder is the T5 v1.1 encoder of
+    f_lite.text_encoder (the 4096-wide context of the 7B / 10B DiTs); any other transformers encoder is called
+    the reference's way (processor -> encoder(..., output_hidden_states=True).hidden_states[-8]) on torch;
+    `prompt_embeds` skips the step.
 """
 from __future__ import annotations
 
@@ -88,11 +90,12 @@ def resolve_dit_class(entry):
 class FLitePipeline:
     model_cpu_offload_seq = "text_encoder->dit_model->vae"
 
-    def __init__(self, dit_model: DiT, vae=None, text_encoder=None, processor=None):
+    def __init__(self, dit_model: DiT, vae=None, text_encoder=None, processor=None, tokenizer=None):
         self.dit_model = dit_model
         self.vae = vae
         self.text_encoder = text_encoder
-        self.processor = processor
+        self.processor = processor if processor is not None else tokenizer  # pt.py:158 passes tokenizer=
+        self.caption_to_text = None  # optional prompt templating hook (the reference's chat template, pipeline.py:105)
         self.vae_scale_factor = 8
         self.return_index = -8
         self._progress_bar_config = {}
@@ -116,13 +119,30 @@ class FLitePipeline:
             from .vae import AutoencoderKL
 
             vae = AutoencoderKL.from_pretrained(root / "vae", torch_dtype=torch_dtype, device=device)
-        return cls(dit, vae)
+        text_encoder, processor = None, None
+        te = root / "text_encoder"
+        if "text_encoder" in index and (te / "config.json").exists():
+            cfg = json.loads((te / "config.json").read_text())
+            if cfg.get("model_type") == "t5":
+                from .text_encoder import T5Encoder
+
+                text_encoder = T5Encoder.from_pretrained(te, torch_dtype=torch_dtype, device=device)
+        for sub in ("tokenizer", "processor"):
+            if sub in index and (root / sub).exists():
+                from transformers import AutoTokenizer
+
+                processor = AutoTokenizer.from_pretrained(str(root / sub), local_files_only=True)
+                break
+        return cls(dit, vae, text_encoder, processor)
 
     def save_pretrained(self, path):
         root = Path(path)
         root.mkdir(parents=True, exist_ok=True)
         index = {"_class_name": "FLitePipeline", "dit_model": [self.dit_model.module_name, "DiT"]}
         self.dit_model.save_pretrained(root / "dit_model")
+        if self.text_encoder is not None and hasattr(self.text_encoder, "save_pretrained"):
+            index["text_encoder"] = ["transformers", "T5EncoderModel"]
+            self.text_encoder.save_pretrained(root / "text_encoder")
         if self.vae is not None:
             index["vae"] = ["diffusers", "AutoencoderKL"]
             self.vae.save_pretrained(root / "vae")
@@ -161,7 +181,7 @@ class FLitePipeline:
         self._progress_bar_config = kwargs
 
     def to(self, torch_device=None, torch_dtype=None, silence_dtype_warnings=False):
-        for m in (self.dit_model, self.vae):
+        for m in (self.dit_model, self.vae, self.text_encoder):
             if m is not None and hasattr(m, "to"):
                 m.to(device=torch_device, dtype=torch_dtype)
         return self
@@ -172,12 +192,36 @@ class FLitePipeline:
 
     def encode_prompt(self, prompt, negative_prompt=None, device=None, dtype=None, max_sequence_length=512,
                       return_index=-8):
-        """pipeline.py:126-175 needs a text encoder; this path takes precomputed embeddings instead."""
+        """pipeline.py:126-175: hidden_states[return_index] of the text encoder over the tokenized prompts
+        (padding "longest" to a multiple of 8, truncation at max_sequence_length); zeros for a missing negative
+        prompt. The native T5 encoder runs only the layers that state needs."""
+        from .text_encoder import T5Encoder
+
         if self.text_encoder is None:
-            raise ValueError("FLitePipeline (MI355X path) needs prompt_embeds: text encoding is out of scope "
-                             "for the native sampling path (pass prompt_embeds / negative_prompt_embeds)")
-        return self.text_encoder.encode_prompt(prompt, negative_prompt, device=device, dtype=dtype,
-                                               max_sequence_length=max_sequence_length, return_index=return_index)
+            raise ValueError("FLitePipeline has no text encoder: pass prompt_embeds / negative_prompt_embeds, or "
+                             "build the pipeline with text_encoder=T5Encoder(...) and its tokenizer")
+        if self.processor is None:
+            raise ValueError("the text encoder needs a tokenizer / processor (FLitePipeline(..., processor=...))")
+        if isinstance(prompt, str):
+            prompt = [prompt]
+        enc = self.text_encoder
+        device = device or enc.device
+        texts = [self.caption_to_text(p) for p in prompt] if self.caption_to_text else list(prompt)
+        tok = self.processor(text=texts, padding="longest", pad_to_multiple_of=8, max_length=max_sequence_length,
+                             truncation=True, return_tensors="pt")
+        if isinstance(enc, T5Encoder):
+            emb = enc.encode(tok["input_ids"], tok.get("attention_mask"), return_index=return_index)
+        else:  # a transformers encoder, called as the reference calls it (pipeline.py:148-154)
+            tok = {k: v.to(device) for k, v in tok.items()}
+            emb = enc(**tok, use_cache=False, return_dict=True, output_hidden_states=True).hidden_states[return_index]
+        dtype = dtype or next(enc.parameters()).dtype
+        emb = emb.to(device=device, dtype=dtype)
+        if negative_prompt is None:
+            neg = torch.zeros_like(emb)
+        else:
+            neg = self.encode_prompt(negative_prompt, device=device, dtype=dtype,
+                                     max_sequence_length=max_sequence_length, return_index=return_index)[0]
+        return emb, neg
 
     # ---------------------------------------------------------------- sampling
     @torch.no_grad()

@@ -33,6 +33,7 @@ int flite_version(void);
 #define FLITE_EPI_STORE_F32 1   /* out_f32[m][n]   = A.W^T + bias                                  */
 #define FLITE_EPI_RESID_F32 2   /* out_f32[m][n]  += gate[m/rows_per_seg][n] * (A.W^T + bias)      */
 #define FLITE_EPI_SWIGLU_BF16 3 /* out_bf16[m][f]  = silu(A.Wg^T)[f] * (A.Wu^T)[f], N = 2F          */
+#define FLITE_EPI_GEGLU_BF16 6  /* out_bf16[m][f]  = gelu_tanh(A.Wg^T)[f] * (A.Wu^T)[f], N = 2F (T5)  */
 
 /*
  * bf16 GEMM with fused epilogue: C[M,N] = A[M,K] . W[N,K]^T  (W in nn.Linear [out,in] layout).
@@ -142,6 +143,24 @@ int flite_rmsnorm_modulate_fp8(void* stream, const float* x, long ldx, void* y8,
 /* Row gather dst[i] = src[idx[i]] (bf16 rows of `cols`, cols % 8 == 0): the context compaction of
  * prepare_flash_attention_inputs (model.py:61-62) for a ragged context_attn_mask. idx: device int32 [n]. */
 int flite_gather_rows(void* stream, const void* src, void* dst, const int* idx, long n, int cols);
+
+/* ---- text encoder (T5 v1.1 encoder; reference pipeline.py:126-175 encode_prompt) ----
+ * Replaces the transformers T5EncoderModel forward the reference calls for prompt embeddings (pt.py:150-155:
+ * the 4096-wide context of cross_attn_input_size = 4096). GEMMs go through flite_gemm_bf16 (GEGLU epilogue
+ * for DenseGatedActDense), norms through flite_rmsnorm_modulate (no modulation).
+ *
+ * Self-attention of one layer (T5Attention, no 1/sqrt(d) scaling): o = softmax(q k^T + bias + mask) v per head
+ * of 64, for L <= 512 tokens per sequence, B sequences of L rows each. bucket: device int32 [2L-1], the
+ * relative-position bucket of (key - query), indexed (key - query + L - 1); rel_weight: layer 0's
+ * relative_attention_bias.weight [num_buckets, H] (bf16); mask: additive fp32 [B, L] over keys (0 keep,
+ * -inf drop) or NULL. q/k/v/o: bf16 rows, head h at column 64 h, row strides in elements. */
+int flite_t5_attention(void* stream, const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                       void* o, long ldo, const int* bucket, const void* rel_weight, const float* mask, int B,
+                       int L, int H);
+
+/* Token-embedding gather into an fp32 residual stream: out[i][:] = float(table[ids[i]][:]) (bf16 table
+ * [vocab, cols], ids clamped to [0, vocab), cols % 4 == 0). */
+int flite_embed_rows_f32(void* stream, const void* table, const int* ids, float* out, long n, int cols, long vocab);
 
 /* TwoDimRotary tables (model.py:334-386) for an (h, w) patch grid with n_reg leading register rows. */
 int flite_rope_tables(void* stream, float* cos_t, float* sin_t, int h, int w, int n_reg, float base, int round_bf16);
