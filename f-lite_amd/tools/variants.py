@@ -18,6 +18,7 @@ PKG = HERE.parent
 sys.path.insert(0, str(PKG))
 
 GEMM_SHAPES = [  # name, M, N, K, epilogue
+    ("cube8k", 8192, 8192, 8192, "store"),
     ("gateup", 8224, 24576, 3072, "swiglu"),
     ("qkv", 8224, 9216, 3072, "store"),
     ("cross_q", 8224, 3072, 3072, "store"),
@@ -26,22 +27,39 @@ GEMM_SHAPES = [  # name, M, N, K, epilogue
 ]
 
 
-def build(src, name, defines):
+def build(src, name, args):
+    """args: -D knobs, and --sub OLD==>NEW textual substitutions applied to a temporary copy of the source
+    (ablation builds: the product source never carries them)."""
     import build_native as bn
 
     bn.build(verbose=False)
     out = HERE / "variants" / name
     out.mkdir(parents=True, exist_ok=True)
+    defines, subs = [], []
+    it = iter(args)
+    for a in it:
+        if a == "--sub":
+            old, new = next(it).split("==>")
+            subs.append((old, new))
+        else:
+            defines.append(a)
+    text = (bn.CSRC / f"{src}.hip").read_text()
+    for old, new in subs:
+        if old not in text:
+            raise SystemExit(f"substitution target not found: {old!r}")
+        text = text.replace(old, new)
+    tmp = out / f"{src}.hip"
+    tmp.write_text(text)
     obj = out / f"{src}.o"
-    cmd = [bn.HIPCC, *bn.CFLAGS, *defines, "-c", str(bn.CSRC / f"{src}.hip"), "-o", str(obj)]
+    cmd = [bn.HIPCC, *bn.CFLAGS, *defines, "-c", str(tmp), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(r.stderr[-4000:])
     objs = [str(obj)] + [str(bn.BUILD / (p.stem + ".o")) for p in bn._sources() if p.stem != src]
     subprocess.run([bn.HIPCC, f"--offload-arch={bn.ARCH}", "-shared", "-fPIC", "-o", str(out / "libflite_hip.so"),
                     *objs], check=True)
-    (out / "defines.json").write_text(json.dumps(defines))
-    print(f"built variant {name}: {defines}")
+    (out / "defines.json").write_text(json.dumps({"defines": defines, "subs": subs}))
+    print(f"built variant {name}: {defines} {len(subs)} substitution(s)")
 
 
 def time_gemms(iters=20):
