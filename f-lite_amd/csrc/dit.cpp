@@ -9,6 +9,8 @@
 
 namespace flite {
 
+constexpr long kPosEmbRows = 2048;  // DiT.positional_embedding rows (model.py:444)
+
 namespace {
 constexpr int HEAD_DIM = 256;
 // q and k are RMS-normalised per head before every DiT attention (QKNorm, model.py:180,197): |q|,|k| <= 16
@@ -146,6 +148,7 @@ int DitEngine::bind(const std::string& name, const void* ptr, long numel) {
   else if (name == "patch_embed.patch_proj.weight") { if (expect(cpp * D)) return 2; w_.patch_w = p; }
   else if (name == "patch_embed.patch_proj.bias") { if (expect(D)) return 2; w_.patch_b = p; }
   else if (name == "register_tokens") { if (expect((long)R * D)) return 2; w_.registers = p; }
+  else if (name == "positional_embedding" && !cfg.use_rope) { if (expect(kPosEmbRows * D)) return 2; w_.pos_emb = p; }
   else if (name == "time_embed.0.weight") { if (expect(4 * DD)) return 2; w_.te0_w = p; }
   else if (name == "time_embed.0.bias") { if (expect(4L * D)) return 2; w_.te0_b = p; }
   else if (name == "time_embed.2.weight") { if (expect(4 * DD)) return 2; w_.te2_w = p; }
@@ -165,6 +168,7 @@ int DitEngine::check_bound() {
   const bool bias = cfg.train_bias_and_rms != 0;
   FLITE_REQUIRE(w_.ctx_proj_w && w_.ctx_proj_b && w_.ctx_norm, "unbound: context_proj/context_norm");
   FLITE_REQUIRE(w_.patch_w && w_.patch_b && w_.registers, "unbound: patch_embed/register_tokens");
+  FLITE_REQUIRE(cfg.use_rope || w_.pos_emb, "unbound: positional_embedding (use_rope = 0)");
   FLITE_REQUIRE(w_.te0_w && w_.te0_b && w_.te2_w && w_.te2_b, "unbound: time_embed");
   FLITE_REQUIRE(w_.fmod_w && w_.fmod_b && w_.fproj_w && w_.fproj_b, "unbound: final stage");
   FLITE_REQUIRE(!bias || w_.fnorm, "unbound: final_norm.weight");
@@ -188,6 +192,8 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   FLITE_REQUIRE(F % 256 == 0 || F % 16 == 0, "config: mlp hidden must be a multiple of 16");
   FLITE_REQUIRE(Hl % P == 0 && Wl % P == 0, "prepare: latent H, W must be multiples of patch_size");
   FLITE_REQUIRE(Hl / P <= 512 && Wl / P <= 512, "prepare: RoPE tables cover at most 512x512 patches");
+  FLITE_REQUIRE(cfg.use_rope || R + (Hl / P) * (Wl / P) <= kPosEmbRows,
+                "prepare: the learned positional embedding covers at most 2048 rows (registers + patches)");
   FLITE_REQUIRE(cfg.cross_attn_input_size % 64 == 0, "config: cross_attn_input_size must be a multiple of 64");
   if (check_bound()) return 2;
   if (B == B_ && Hl == Hl_ && Wl == Wl_ && n_ctx_max <= nctx_max_ && n_t_max <= ntmax_) return 0;
@@ -450,7 +456,8 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.rope_cos = cos_;
     g.rope_sin = sin_;
     g.rope_tokens = T_;
-    g.rope_cols = g.norm_cols = 2 * D;
+    g.norm_cols = 2 * D;
+    g.rope_cols = cfg.use_rope ? 2 * D : 0;
     if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
     if (gemm(g, fuse_qk_norm() ? EPI_QKV_NORM_BF16 : EPI_STORE_BF16, s)) return 1;
     if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
@@ -461,7 +468,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     rn.ldx = 3L * D;
     rn.rows = M_;
     rn.heads = 2 * H;  // q heads then k heads ("(k h d)" layout, model.py:163)
-    rn.rope_heads = 2 * H;
+    rn.rope_heads = cfg.use_rope ? 2 * H : 0;
     rn.cos = cos_;
     rn.sin = sin_;
     rn.tokens_per_seq = T_;
@@ -717,7 +724,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   if (g8(nbuf8_, nbuf8_s_, q.qkv, q.qkv_s, 3L * D, 3 * D, D, b.qkv_b, EPI8_STORE_BF16, qkv_, 3L * D, nullptr))
     return 1;
   if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
-  if (qk_norm(3L * D, 2 * H, 2 * H)) return 1;
+  if (qk_norm(3L * D, 2 * H, cfg.use_rope ? 2 * H : 0)) return 1;
   if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
   if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, T_)) return 1;
   if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
@@ -805,6 +812,8 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     if (gemm(g, EPI_STORE_F32, s)) return 1;
   }
   if (fill_registers(x_, w_.registers, B_, T_, R, D, s)) return 1;
+  // use_rope = False: x + positional_embedding[:, :T] over the register + patch rows (model.py:546)
+  if (!cfg.use_rope && add_pos_embed(x_, w_.pos_emb, B_, T_, D, s)) return 1;
   const long mseg = (long)t_row_step * mod_t_stride_;
   for (int i = 0; i < cfg.depth; ++i) {
     const float* mod = mod_ + (long)t_row0 * mod_t_stride_ + (cfg.per_block_adaln ? (long)i * 9 * D : 0);

@@ -25,6 +25,7 @@ struct BlockW {
 struct DitW {
   const bf16_t *ctx_proj_w = nullptr, *ctx_proj_b = nullptr, *ctx_norm = nullptr;
   const bf16_t *patch_w = nullptr, *patch_b = nullptr, *registers = nullptr;
+  const bf16_t* pos_emb = nullptr;  // positional_embedding [1, 2048, D] (use_rope = 0)
   const bf16_t *te0_w = nullptr, *te0_b = nullptr, *te2_w = nullptr, *te2_b = nullptr;
   const bf16_t *ada_w = nullptr, *ada_b = nullptr;  // shared adaLN (model.py layout)
   const bf16_t *fmod_w = nullptr, *fmod_b = nullptr, *fnorm = nullptr, *fproj_w = nullptr, *fproj_b = nullptr;

@@ -277,6 +277,13 @@ __global__ __launch_bounds__(256) void fill_registers_kernel(float* x, const bf1
   }
 }
 
+// x[b][t] += positional_embedding[t] for every row t of every sample (use_rope = False, model.py:546)
+__global__ __launch_bounds__(256) void add_pos_embed_kernel(float* x, const bf16_t* pos, int B, int T, int D) {
+  const long total = (long)B * T * D;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x)
+    x[idx] += bf2f(pos[idx % ((long)T * D)]);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Unpatchify + classifier-free guidance + Euler update (pipeline.py:274,290,296-297; model.py:583-590).
 //   out rows = [dup*Bi*HW, C*p*p] fp32 with columns (p1, p2, c); image i uses rows of copy 0 (uncond)
@@ -571,6 +578,13 @@ int patchify(const void* lat, bool in_bf16, bf16_t* out, int Bi, int C, int H, i
 
 int fill_registers(float* x, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s) {
   hipLaunchKernelGGL(fill_registers_kernel, dim3(grid_for((long)B * R * D)), dim3(256), 0, s, x, reg, B, T, R, D);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int add_pos_embed(float* x, const bf16_t* pos, int B, int T, int D, hipStream_t s) {
+  FLITE_REQUIRE(pos != nullptr, "add_pos_embed: positional_embedding not bound");
+  hipLaunchKernelGGL(add_pos_embed_kernel, dim3(grid_for((long)B * T * D)), dim3(256), 0, s, x, pos, B, T, D);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

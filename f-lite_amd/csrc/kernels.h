@@ -126,6 +126,7 @@ int rope_qknorm(const RopeNormParams& p, hipStream_t s);
 
 int patchify(const void* lat, bool in_bf16, bf16_t* out, int Bi, int C, int H, int W, int P, int dup, hipStream_t s);
 int fill_registers(float* x, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s);
+int add_pos_embed(float* x, const bf16_t* pos, int B, int T, int D, hipStream_t s);
 int cfg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, int dup, float g, float dt,
               hipStream_t s);
 int cfg_euler_nchw(const float* u, const float* c, float* acc, long n, float g, float dt, int use_cfg,

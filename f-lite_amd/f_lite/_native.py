@@ -46,6 +46,7 @@ class DitConfig(ctypes.Structure):
         ("rope_base", _f),
         ("bf16_timestep_quant", _i),
         ("bf16_rope_tables", _i),
+        ("use_rope", _i),
     ]
 
 

@@ -272,12 +272,11 @@ class DiT(nn.Module):
         cfg.rope_base = float(c.rope_base)
         cfg.bf16_timestep_quant = int(self.dtype == torch.bfloat16)
         cfg.bf16_rope_tables = int(self.dtype == torch.bfloat16)
+        cfg.use_rope = int(bool(c.use_rope))
         return cfg
 
     def engine(self) -> _native.DitEngine:
         """The native engine with every parameter bound (re-binds when parameter storage moved)."""
-        if not self.config.use_rope:
-            raise NotImplementedError("use_rope=False (learned positional embedding) is not on the native path")
         params = list(self.named_parameters())
         if not params[0][1].is_cuda:
             raise _native.FliteError("DiT parameters are on the CPU: the F-Lite path runs only on a ROCm device "

@@ -196,6 +196,8 @@ typedef struct flite_dit_config {
   float rope_base;            /* rope_base                                    */
   int bf16_timestep_quant;    /* 1 = bf16 model semantics for t  */
   int bf16_rope_tables;       /* 1 = RoPE tables rounded to bf16 (bf16 model) */
+  int use_rope;               /* 1 = 2-D RoPE (model.py:537-544); 0 = learned positional_embedding
+                                 [1, 2048, D] added to the register+patch rows (model.py:444,546), no RoPE */
 } flite_dit_config;
 
 typedef struct flite_dit flite_dit;

@@ -158,6 +158,7 @@ class DiTConfig:
     train_bias_and_rms: bool = True
     rope_base: float = 10000.0
     per_block_adaln: bool = False  # model_v2.py layout
+    use_rope: bool = True  # False: learned positional_embedding (model.py:444,546), no RoPE
 
     def as_dict(self):
         return dict(self.__dict__)
@@ -223,8 +224,9 @@ class RefDiT:
         L = qkv.shape[0]
         qkv = qkv.reshape(L, 3, H, -1).permute(1, 2, 0, 3)  # "l (k h d) -> k h l d"
         q, k, v = qkv.unbind(0)
-        q = apply_rotary_emb(q, cos, sin)
-        k = apply_rotary_emb(k, cos, sin)
+        if cos is not None:  # use_rope (model.py:166-167 applies RoPE only when given)
+            q = apply_rotary_emb(q, cos, sin)
+            k = apply_rotary_emb(k, cos, sin)
         q = own_rmsnorm(q, None)
         k = own_rmsnorm(k, None)
         q, k, v = (t.transpose(0, 1) for t in (q, k, v))  # "h l d -> l h d"
@@ -271,9 +273,13 @@ class RefDiT:
         xe = xe.flatten(2).transpose(1, 2)  # "b c h w -> b (h w) c"
         xe = torch.cat([self.p["register_tokens"].repeat(b, 1, 1), xe], 1)
         T = xe.shape[1]
-        cos, sin = rope_tables(h // p, w // p, D // (2 * c.num_heads), c.rope_base, 16, self.rope_dtype)
-        cos = cos[None].repeat(1, b, 1)
-        sin = sin[None].repeat(1, b, 1)
+        if c.use_rope:  # model.py:537-544
+            cos, sin = rope_tables(h // p, w // p, D // (2 * c.num_heads), c.rope_base, 16, self.rope_dtype)
+            cos = cos[None].repeat(1, b, 1)
+            sin = sin[None].repeat(1, b, 1)
+        else:  # model.py:546
+            xe = xe + self.p["positional_embedding"].repeat(b, 1, 1)[:, :T, :]
+            cos, sin = None, None
         x_flat, cu, maxl, idx = prepare_varlen(xe)
         t_emb = self.t_embed(timesteps)
         st = F.silu(t_emb)

@@ -81,6 +81,8 @@ def param_shapes(cfg: dict) -> "dict[str, tuple]":
     s["patch_embed.patch_proj.weight"] = (D, C, p, p)
     s["patch_embed.patch_proj.bias"] = (D,)
     s["register_tokens"] = (1, 16, D)
+    if not cfg.get("use_rope", True):
+        s["positional_embedding"] = (1, 2048, D)  # model.py:444
     s["time_embed.0.weight"] = (4 * D, D)
     s["time_embed.0.bias"] = (4 * D,)
     s["time_embed.2.weight"] = (D, 4 * D)

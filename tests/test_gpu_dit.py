@@ -52,6 +52,25 @@ def test_forward_matches_golden_and_oracle(golden, tiny, tiny_ref):
     assert psnr(out, golden["dit.tiny.f32.nomask"]) >= 35.0
 
 
+@pytest.mark.parametrize("preset", ["tiny", "tiny_v2"])
+def test_forward_learned_positional_embedding(golden, preset):
+    """use_rope=False (model.py:444,546): x + positional_embedding[:, :T] after the registers, no RoPE."""
+    import dataclasses
+
+    m = DiT.random(seed=0, **PRESETS[preset], use_rope=False)
+    x, ctx = _inputs(golden)
+    t = golden["in.t"]
+    out = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32)
+    cfg = dataclasses.replace(R.PRESETS[preset], use_rope=False)
+    ref = R.RefDiT.random(cfg, dtype=torch.float32)(x.float(), ctx.float(), None, t)
+    p = psnr(out, ref)
+    print(f"{preset} use_rope=False forward PSNR vs fp32 oracle: {p:.2f} dB")
+    assert p >= 40.0
+    # the embedding matters: the RoPE model on the same weights is far from it
+    rope = DiT.random(seed=0, **PRESETS[preset])(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32)
+    assert psnr(rope, ref) < p - 10
+
+
 def test_forward_three_arg_form(golden, tiny):
     x, ctx = _inputs(golden)
     t = golden["in.t"].to(DEV)

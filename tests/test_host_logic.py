@@ -32,6 +32,17 @@ def test_state_dict_inventory_matches_reference(name):
     assert all(tuple(sd[k].shape) == tuple(ref[k]) for k in ref)
 
 
+@pytest.mark.parametrize("name", ["tiny", "tiny_v2"])
+def test_state_dict_inventory_learned_positional_embedding(name):
+    """use_rope=False adds positional_embedding [1, 2048, D] (model.py:444)."""
+    with torch.device("meta"):
+        m = DiT(**PRESETS[name], use_rope=False)
+    sd = m.state_dict()
+    ref = param_shapes(dict(PRESETS[name], use_rope=False))
+    assert "positional_embedding" in ref and set(sd) == set(ref)
+    assert all(tuple(sd[k].shape) == tuple(ref[k]) for k in ref)
+
+
 def test_reference_ctor_defaults():
     with torch.device("meta"):
         m = DiT()
