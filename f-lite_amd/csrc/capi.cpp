@@ -202,6 +202,21 @@ int flite_dit_create(const flite_dit_config* cfg, flite_dit** out) {
   return 0;
 }
 
+int flite_dit_set_sequence_parallel(flite_dit* dit, int rank, int nranks, flite_sp_allgather_fn fn, void* user) {
+  FLITE_REQUIRE(dit != nullptr, "flite_dit_set_sequence_parallel: null engine");
+  return dit->eng->set_sequence_parallel(rank, nranks, fn, user);
+}
+
+int flite_dit_sp_buffer_bytes(flite_dit* dit, long* kv_send_bytes, long* out_send_bytes) {
+  FLITE_REQUIRE(dit && kv_send_bytes && out_send_bytes, "flite_dit_sp_buffer_bytes: null argument");
+  return dit->eng->sp_buffer_bytes(kv_send_bytes, out_send_bytes);
+}
+
+int flite_dit_sp_bind_buffers(flite_dit* dit, void* kv_send, void* kv_recv, void* out_send, void* out_recv) {
+  FLITE_REQUIRE(dit != nullptr, "flite_dit_sp_bind_buffers: null engine");
+  return dit->eng->sp_bind_buffers(kv_send, kv_recv, out_send, out_recv);
+}
+
 int flite_dit_destroy(flite_dit* dit) {
   if (dit) {
     delete dit->eng;

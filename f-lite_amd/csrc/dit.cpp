@@ -72,6 +72,9 @@ void DitEngine::free_ws() {
   attn_ws_ = nullptr;
   attn_ws_bytes_ = 0;
   nbuf8_ = nbuf8_s_ = obuf8_ = obuf8_s_ = hbuf8_ = hbuf8_s_ = nullptr;
+  x_ = nullptr;
+  kv_full_ = nullptr;
+  cu_full_ = nullptr;
 }
 
 void DitEngine::free_fp8_weights() {
@@ -196,6 +199,8 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
                 "prepare: the learned positional embedding covers at most 2048 rows (registers + patches)");
   FLITE_REQUIRE(cfg.cross_attn_input_size % 64 == 0, "config: cross_attn_input_size must be a multiple of 64");
   if (check_bound()) return 2;
+  FLITE_REQUIRE(sp_n_ == 1 || (!fp8_ && cfg.use_rope),
+                "prepare: sequence parallelism runs the bf16 RoPE path only (no fp8, no positional_embedding)");
   if (B == B_ && Hl == Hl_ && Wl == Wl_ && n_ctx_max <= nctx_max_ && n_t_max <= ntmax_) return 0;
   drop_graph();
   free_ws();
@@ -204,7 +209,11 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   Wl_ = Wl;
   HW_ = (Hl / P) * (Wl / P);
   T_ = R + HW_;
-  M_ = (long)B * T_;
+  Tl_ = (T_ + sp_n_ - 1) / sp_n_;
+  FLITE_REQUIRE(Tl_ >= R, "prepare: sequence parallelism needs at least 16 rows per rank");
+  M_ = (long)B * Tl_;
+  sp_kv_send_ = sp_kv_recv_ = nullptr;  // caller buffers are sized per shape: bind again after prepare
+  sp_out_send_ = sp_out_recv_ = nullptr;
   nctx_max_ = n_ctx_max;
   ntmax_ = n_t_max;
   const int cpp = C * P * P;
@@ -231,8 +240,18 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   }
   if (alloc((void**)&cu_self_, (B + 1) * 4)) return 1;
   if (alloc((void**)&cu_ctx_, (B + 1) * 4)) return 1;
-  if (alloc((void**)&cos_, (long)T_ * 128 * 4)) return 1;
-  if (alloc((void**)&sin_, (long)T_ * 128 * 4)) return 1;
+  // RoPE tables for every row a rank may hold (the last rank's padding rows read zeros)
+  if (alloc((void**)&cos_, (long)sp_n_ * Tl_ * 128 * 4)) return 1;
+  if (alloc((void**)&sin_, (long)sp_n_ * Tl_ * 128 * 4)) return 1;
+  FLITE_HIP_CHECK(hipMemset(cos_, 0, (size_t)sp_n_ * Tl_ * 128 * 4));
+  FLITE_HIP_CHECK(hipMemset(sin_, 0, (size_t)sp_n_ * Tl_ * 128 * 4));
+  if (sp_n_ > 1) {
+    if (alloc((void**)&kv_full_, (long)B * T_ * 2 * D * 2)) return 1;
+    if (alloc((void**)&cu_full_, (B + 1) * 4)) return 1;
+    std::vector<int> cuf(B + 1);
+    for (int i = 0; i <= B; ++i) cuf[i] = i * T_;
+    FLITE_HIP_CHECK(hipMemcpy(cu_full_, cuf.data(), (B + 1) * 4, hipMemcpyHostToDevice));
+  }
   if (alloc((void**)&inv_freq_, 64 * 4)) return 1;
   if (alloc((void**)&ctx_p_, (long)std::max(n_ctx_max, 1) * D * 2)) return 1;
   ctx_kv_.assign(cfg.depth, nullptr);
@@ -249,7 +268,7 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
 
   // self-attention cu_seqlens [0, T, 2T, ...] (prepare_flash_attention_inputs with no mask, model.py:549)
   std::vector<int> cu(B + 1);
-  for (int i = 0; i <= B; ++i) cu[i] = i * T_;
+  for (int i = 0; i <= B; ++i) cu[i] = i * Tl_;  // queries held here
   FLITE_HIP_CHECK(hipMemcpy(cu_self_, cu.data(), (B + 1) * 4, hipMemcpyHostToDevice));
   // RoPE inv_freq in double like the reference's python list (model.py:342), then fp32
   const int rdim = D / (2 * H);  // 128
@@ -416,8 +435,8 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     nm.mod_seg_stride = mseg;
     nm.rows = M_;
     nm.D = D;
-    nm.in_seg = T_;
-    nm.in_stride = T_;
+    nm.in_seg = Tl_;
+    nm.in_stride = Tl_;
     nm.in_off = 0;
     return rmsnorm_mod(nm, false, s);
   };
@@ -431,12 +450,13 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.ldo = D;
     g.gate = gate;
     g.gate_seg_stride = mseg;
-    g.rows_per_seg = T_;
+    g.rows_per_seg = Tl_;
     g.M = (int)M_;
     g.N = D;
     g.K = K;
     return gemm(g, EPI_RESID_F32, s);
   };
+  const long rope_off = (long)sp_rank_ * Tl_ * 128;  // table rows of the tokens held here
 
   // --- self attention ---
   if (norm(b.norm1, shift_sa, scale_sa)) return 1;
@@ -453,9 +473,9 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.N = 3 * D;
     g.K = D;
     // RoPE + QK-norm of the q and k heads ("(k h d)" layout, model.py:163) in the GEMM epilogue
-    g.rope_cos = cos_;
-    g.rope_sin = sin_;
-    g.rope_tokens = T_;
+    g.rope_cos = cos_ + rope_off;
+    g.rope_sin = sin_ + rope_off;
+    g.rope_tokens = Tl_;
     g.norm_cols = 2 * D;
     g.rope_cols = cfg.use_rope ? 2 * D : 0;
     if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
@@ -469,26 +489,28 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     rn.rows = M_;
     rn.heads = 2 * H;  // q heads then k heads ("(k h d)" layout, model.py:163)
     rn.rope_heads = cfg.use_rope ? 2 * H : 0;
-    rn.cos = cos_;
-    rn.sin = sin_;
-    rn.tokens_per_seq = T_;
+    rn.cos = cos_ + rope_off;
+    rn.sin = sin_ + rope_off;
+    rn.tokens_per_seq = Tl_;
     if (rope_qknorm(rn, s)) return 1;
   }
+  if (sp_n_ > 1 && sp_gather_kv(s)) return 1;  // every key of the sequence (normed, rotated) on every rank
   {
     AttnParams a;
     a.q = qkv_;
-    a.k = qkv_ + D;
-    a.v = qkv_ + 2L * D;
+    a.k = sp_n_ > 1 ? kv_full_ : qkv_ + D;
+    a.v = sp_n_ > 1 ? kv_full_ + D : qkv_ + 2L * D;
     a.o = obuf_;
-    a.q_row_stride = a.k_row_stride = a.v_row_stride = 3L * D;
+    a.q_row_stride = 3L * D;
+    a.k_row_stride = a.v_row_stride = sp_n_ > 1 ? 2L * D : 3L * D;
     a.o_row_stride = D;
     a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = HEAD_DIM;
     a.cu_q = cu_self_;
-    a.cu_k = cu_self_;
+    a.cu_k = sp_n_ > 1 ? cu_full_ : cu_self_;
     a.B = B_;
     a.H = H;
     a.head_dim = HEAD_DIM;
-    a.max_q = T_;
+    a.max_q = Tl_;
     a.max_k = T_;
     a.scale = 1.0f / sqrtf((float)HEAD_DIM);
     a.max_score = kQKNormScoreBound;
@@ -539,7 +561,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.B = B_;
     a.H = H;
     a.head_dim = HEAD_DIM;
-    a.max_q = T_;
+    a.max_q = Tl_;
     a.max_k = ctx_max_len_;
     a.scale = 1.0f / sqrtf((float)HEAD_DIM);
     a.max_score = kQKNormScoreBound;
@@ -596,6 +618,7 @@ int DitEngine::enable_fp8(hipStream_t s, bool on) {
     fp8_ = false;
     return 0;
   }
+  FLITE_REQUIRE(sp_n_ == 1, "enable_fp8: not with sequence parallelism");
   if (check_bound()) return 2;
   FLITE_REQUIRE(D % 128 == 0 && F % 128 == 0, "fp8: hidden and MLP widths must be multiples of 128");
   if (w8_.empty()) {
@@ -649,8 +672,8 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     nm.mod_seg_stride = mseg;
     nm.rows = M_;
     nm.D = D;
-    nm.in_seg = T_;
-    nm.in_stride = T_;
+    nm.in_seg = Tl_;
+    nm.in_stride = Tl_;
     nm.in_off = 0;
     return rmsnorm_mod(nm, false, s);
   };
@@ -670,7 +693,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     g.ldo = ldo;
     g.gate = gate;
     g.gate_seg_stride = mseg;
-    g.rows_per_seg = T_;
+    g.rows_per_seg = Tl_;
     g.M = (int)M_;
     g.N = N;
     g.K = K;
@@ -696,7 +719,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     a.B = B_;
     a.H = H;
     a.head_dim = HEAD_DIM;
-    a.max_q = T_;
+    a.max_q = Tl_;
     a.max_k = max_k;
     a.scale = 1.0f / sqrtf((float)HEAD_DIM);
     a.max_score = kQKNormScoreBound;
@@ -714,7 +737,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     if (rope_heads > 0) {
       rn.cos = cos_;
       rn.sin = sin_;
-      rn.tokens_per_seq = T_;
+      rn.tokens_per_seq = Tl_;
     }
     return rope_qknorm(rn, s);
   };
@@ -726,7 +749,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
   if (qk_norm(3L * D, 2 * H, cfg.use_rope ? 2 * H : 0)) return 1;
   if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
-  if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, T_)) return 1;
+  if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, Tl_)) return 1;
   if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
   if (quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
   if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa)) return 1;
@@ -791,10 +814,34 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
   FLITE_REQUIRE(Bi * dup == B_, "forward: batch does not match the prepared workspace");
   FLITE_REQUIRE(nseq_ctx_ == B_, "forward: set_context must be called for this batch");
   FLITE_REQUIRE(t_row0 >= 0 && t_row0 + (B_ - 1) * t_row_step < nt_, "forward: timestep rows out of range");
+  FLITE_REQUIRE(sp_n_ == 1 || (sp_kv_send_ && sp_kv_recv_ && sp_out_send_ && sp_out_recv_),
+                "forward: sequence parallelism needs its exchange buffers (flite_dit_sp_bind_buffers)");
   const int cpp = C * P * P;
   // patch embed (model.py:533) straight into the residual stream after the registers (model.py:535)
   if (patchify(lat, lat_bf16, patches_, Bi, C, Hl_, Wl_, P, dup, s)) return 1;
-  {
+  if (sp_n_ > 1) {
+    // rows [r0, r0 + Tl) of each sequence: patches [p0, p1) land at local rows p + R - r0
+    const int r0 = sp_rank_ * Tl_, t_hi = std::min(T_, r0 + Tl_);
+    const int p0 = std::max(r0 - R, 0), p1 = t_hi - R;
+    if (t_hi < r0 + Tl_)  // padding rows of the last rank: keep them finite
+      FLITE_HIP_CHECK(hipMemset2DAsync(x_ + (long)(t_hi - r0) * D, (size_t)Tl_ * D * 4, 0,
+                                       (size_t)(r0 + Tl_ - t_hi) * D * 4, B_, s));
+    for (int b = 0; b < B_ && p1 > p0; ++b) {
+      GemmParams g;
+      g.A = patches_ + ((long)b * HW_ + p0) * cpp;
+      g.lda = cpp;
+      g.W = w_.patch_w;
+      g.ldw = cpp;
+      g.bias = w_.patch_b;
+      g.out = x_ + ((long)b * Tl_ + (p0 + R - r0)) * D;
+      g.ldo = D;
+      g.M = p1 - p0;
+      g.N = D;
+      g.K = cpp;
+      if (gemm(g, EPI_STORE_F32, s)) return 1;
+    }
+    if (r0 == 0 && fill_registers(x_, w_.registers, B_, Tl_, R, D, s)) return 1;
+  } else {
     GemmParams g;
     g.A = patches_;
     g.lda = cpp;
@@ -810,8 +857,8 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     g.out_seg_stride = T_;
     g.out_seg_off = R;
     if (gemm(g, EPI_STORE_F32, s)) return 1;
+    if (fill_registers(x_, w_.registers, B_, T_, R, D, s)) return 1;
   }
-  if (fill_registers(x_, w_.registers, B_, T_, R, D, s)) return 1;
   // use_rope = False: x + positional_embedding[:, :T] over the register + patch rows (model.py:546)
   if (!cfg.use_rope && add_pos_embed(x_, w_.pos_emb, B_, T_, D, s)) return 1;
   const long mseg = (long)t_row_step * mod_t_stride_;
@@ -830,11 +877,13 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     nm.shift = fmod_ + (long)t_row0 * 2 * D;
     nm.scale = fmod_ + (long)t_row0 * 2 * D + D;
     nm.mod_seg_stride = (long)t_row_step * 2 * D;
-    nm.rows = (long)B_ * HW_;
+    // sequence parallel: every row held here (registers and padding included, dropped by the gather)
+    const bool sp = sp_n_ > 1;
+    nm.rows = sp ? M_ : (long)B_ * HW_;
     nm.D = D;
-    nm.in_seg = HW_;
-    nm.in_stride = T_;
-    nm.in_off = R;
+    nm.in_seg = sp ? Tl_ : HW_;
+    nm.in_stride = sp ? Tl_ : T_;
+    nm.in_off = sp ? 0 : R;
     if (rmsnorm_mod(nm, false, s)) return 1;
     GemmParams g;
     g.A = nbuf_;
@@ -842,13 +891,72 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     g.W = w_.fproj_w;
     g.ldw = D;
     g.bias = w_.fproj_b;
-    g.out = fout_;
+    g.out = sp ? sp_out_send_ : fout_;
     g.ldo = cpp;
-    g.M = B_ * HW_;
+    g.M = sp ? (int)M_ : B_ * HW_;
     g.N = cpp;
     g.K = D;
     if (gemm(g, EPI_STORE_F32, s)) return 1;
+    if (sp && sp_gather_out(s)) return 1;
   }
+  return 0;
+}
+
+// K/V rows of this rank -> every rank's, reordered into whole sequences [B][T][2D] (kv_full_)
+int DitEngine::sp_gather_kv(hipStream_t s) {
+  const size_t row = 2 * (size_t)D * 2;
+  FLITE_HIP_CHECK(hipMemcpy2DAsync(sp_kv_send_, row, qkv_ + D, 3 * (size_t)D * 2, row, M_, hipMemcpyDeviceToDevice, s));
+  FLITE_REQUIRE(sp_fn_(sp_user_, 0, (void*)s) == 0, "sequence parallel: K/V exchange failed");
+  for (int q = 0; q < sp_n_; ++q) {
+    const int valid = std::min(T_, (q + 1) * Tl_) - q * Tl_;
+    if (valid <= 0) continue;
+    FLITE_HIP_CHECK(hipMemcpy2DAsync(kv_full_ + (long)q * Tl_ * 2 * D, (size_t)T_ * row,
+                                     sp_kv_recv_ + (long)q * M_ * 2 * D, (size_t)Tl_ * row, (size_t)valid * row, B_,
+                                     hipMemcpyDeviceToDevice, s));
+  }
+  return 0;
+}
+
+// final-projection rows of every rank -> the model output [B][HW][C p p] (fout_), registers and padding dropped
+int DitEngine::sp_gather_out(hipStream_t s) {
+  const size_t row = (size_t)C * P * P * 4;
+  FLITE_REQUIRE(sp_fn_(sp_user_, 1, (void*)s) == 0, "sequence parallel: output exchange failed");
+  for (int q = 0; q < sp_n_; ++q) {
+    const int t_lo = std::max(q * Tl_, R), t_hi = std::min(T_, (q + 1) * Tl_);
+    if (t_hi <= t_lo) continue;
+    FLITE_HIP_CHECK(hipMemcpy2DAsync((char*)fout_ + (size_t)(t_lo - R) * row, (size_t)HW_ * row,
+                                     (const char*)sp_out_recv_ + ((size_t)q * M_ + (t_lo - q * Tl_)) * row,
+                                     (size_t)Tl_ * row, (size_t)(t_hi - t_lo) * row, B_, hipMemcpyDeviceToDevice, s));
+  }
+  return 0;
+}
+
+int DitEngine::set_sequence_parallel(int rank, int nranks, flite_sp_allgather_fn fn, void* user) {
+  FLITE_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "sequence parallel: bad rank / nranks");
+  FLITE_REQUIRE(nranks == 1 || fn != nullptr, "sequence parallel: exchange callback missing");
+  sp_rank_ = rank;
+  sp_n_ = nranks;
+  sp_fn_ = fn;
+  sp_user_ = user;
+  drop_graph();
+  free_ws();
+  B_ = Hl_ = Wl_ = 0;  // the next prepare lays out the rows of this rank
+  return 0;
+}
+
+int DitEngine::sp_buffer_bytes(long* kv_send, long* out_send) const {
+  FLITE_REQUIRE(x_ != nullptr, "sp_buffer_bytes: call prepare first");
+  *kv_send = M_ * 2 * D * 2;
+  *out_send = M_ * (long)C * P * P * 4;
+  return 0;
+}
+
+int DitEngine::sp_bind_buffers(void* kv_send, void* kv_recv, void* out_send, void* out_recv) {
+  FLITE_REQUIRE(kv_send && kv_recv && out_send && out_recv, "sp_bind_buffers: null buffer");
+  sp_kv_send_ = (bf16_t*)kv_send;
+  sp_kv_recv_ = (bf16_t*)kv_recv;
+  sp_out_send_ = (float*)out_send;
+  sp_out_recv_ = (float*)out_recv;
   return 0;
 }
 
@@ -880,7 +988,7 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
     }
     return 0;
   };
-  if (!use_graph) return body(s, acc);
+  if (!use_graph || sp_n_ > 1) return body(s, acc);  // the host exchange callback cannot be captured
 
   // hipGraph: capture the whole n_steps loop once per (shape, schedule, guidance), replay after. The graph
   // integrates into the engine-owned accumulator acc_, so the caller's buffer address does not key the graph.

@@ -51,6 +51,11 @@ class DitEngine {
   // fp8 mode (flite_dit_enable_fp8): MXFP8 copies of the block GEMM weights + fp8 activations
   int enable_fp8(hipStream_t s, bool on);
 
+  // sequence parallelism (flite_dit_set_sequence_parallel)
+  int set_sequence_parallel(int rank, int nranks, flite_sp_allgather_fn fn, void* user);
+  int sp_buffer_bytes(long* kv_send, long* out_send) const;
+  int sp_bind_buffers(void* kv_send, void* kv_recv, void* out_send, void* out_recv);
+
   const flite_dit_config cfg;
   int D, H, F, R, P, C;
 
@@ -67,6 +72,8 @@ class DitEngine {
   int probe_n_ = 0;
 
   int run_block(hipStream_t s, int blk, const float* mod, long mseg);
+  int sp_gather_kv(hipStream_t s);
+  int sp_gather_out(hipStream_t s);
   int run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg);
   int alloc_fp8_act();
   void free_fp8_weights();
@@ -80,6 +87,14 @@ class DitEngine {
   std::vector<void*> allocs_;
   // shape
   int B_ = 0, Hl_ = 0, Wl_ = 0, T_ = 0, HW_ = 0, ntmax_ = 0, nctx_max_ = 0;
+  int Tl_ = 0;  // rows of each sequence held here (T_ without sequence parallelism)
+  // sequence parallelism
+  int sp_rank_ = 0, sp_n_ = 1;
+  flite_sp_allgather_fn sp_fn_ = nullptr;
+  void* sp_user_ = nullptr;
+  bf16_t *sp_kv_send_ = nullptr, *sp_kv_recv_ = nullptr, *kv_full_ = nullptr;
+  float *sp_out_send_ = nullptr, *sp_out_recv_ = nullptr;
+  int *cu_full_ = nullptr;
   long M_ = 0;
   int nctx_ = 0, nseq_ctx_ = 0, ctx_max_len_ = 0;
   // workspace

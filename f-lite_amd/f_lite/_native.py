@@ -94,6 +94,9 @@ SIGNATURES = {
                             _i]),
     "flite_rmsnorm_modulate_fp8": (_i, [_vp, _vp, _l, _vp, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_dit_enable_fp8": (_i, [_vp, _vp, _i]),
+    "flite_dit_set_sequence_parallel": (_i, [_vp, _i, _i, _vp, _vp]),
+    "flite_dit_sp_buffer_bytes": (_i, [_vp, ctypes.POINTER(_l), ctypes.POINTER(_l)]),
+    "flite_dit_sp_bind_buffers": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "flite_dit_set_probe": (_i, [_vp, _i, _i]),
     "flite_dit_read_probe": (_i, [_vp, ctypes.POINTER(_f), _i, ctypes.POINTER(_i)]),
 }
@@ -387,6 +390,9 @@ def gather_rows(src, idx, out=None):
     return out
 
 
+SP_ALLGATHER_FN = ctypes.CFUNCTYPE(_i, _vp, _i, _vp)  # flite_sp_allgather_fn
+
+
 class DitEngine:
     """Owner of a native flite_dit handle (the DiT forward and the denoise loop in C++)."""
 
@@ -395,6 +401,38 @@ class DitEngine:
         self.h = _vp()
         check(self.lib.flite_dit_create(ctypes.byref(cfg), ctypes.byref(self.h)), "flite_dit_create")
         self.cfg = cfg
+        self._sp = None  # (rank, nranks, allgather) with sequence parallelism
+        self._sp_cb = None
+        self._sp_bufs = None
+        self._sp_error = None
+        self._device = None
+
+    def set_sequence_parallel(self, rank: int = 0, nranks: int = 1, allgather=None):
+        """flite_dit_set_sequence_parallel: this engine computes rows [rank*Tl, (rank+1)*Tl) of every sequence.
+        allgather(send, recv) must all-gather the uint8 device tensor `send` into `recv` (nranks x, rank order)
+        on the current stream. nranks = 1 switches back to the whole sequence. Call prepare() afterwards."""
+        if nranks > 1:
+            if allgather is None:
+                raise FliteError("sequence parallelism needs an allgather(send, recv) exchange")
+
+            def cb(user, which, stream):
+                try:
+                    send, recv = self._sp_bufs[which]
+                    allgather(send, recv)
+                    return 0
+                except Exception as e:  # reported by the failing flite call
+                    self._sp_error = e
+                    return 1
+
+            self._sp_cb = SP_ALLGATHER_FN(cb)
+            fn = self._sp_cb
+            self._sp = (rank, nranks, allgather)
+        else:
+            fn = ctypes.cast(None, SP_ALLGATHER_FN)
+            self._sp, self._sp_cb = None, None
+        self._sp_bufs = None
+        check(self.lib.flite_dit_set_sequence_parallel(self.h, rank, nranks, fn, None),
+              "flite_dit_set_sequence_parallel")
 
     def __del__(self):
         try:
@@ -407,8 +445,19 @@ class DitEngine:
         require_gpu(t, name, torch.bfloat16)
         check(self.lib.flite_dit_bind(self.h, name.encode(), t.data_ptr(), t.numel()), f"bind({name})")
 
-    def prepare(self, batch, lat_h, lat_w, n_ctx, n_t):
+    def prepare(self, batch, lat_h, lat_w, n_ctx, n_t, device=None):
         check(self.lib.flite_dit_prepare(self.h, batch, lat_h, lat_w, n_ctx, n_t), "flite_dit_prepare")
+        if self._sp is not None:  # (re)bind the exchange buffers for this shape
+            kv, out = _l(0), _l(0)
+            check(self.lib.flite_dit_sp_buffer_bytes(self.h, ctypes.byref(kv), ctypes.byref(out)),
+                  "flite_dit_sp_buffer_bytes")
+            n = self._sp[1]
+            dev = device or torch.device("cuda", torch.cuda.current_device())
+            mk = lambda b: torch.empty(b, dtype=torch.uint8, device=dev)  # noqa: E731
+            self._sp_bufs = ((mk(kv.value), mk(n * kv.value)), (mk(out.value), mk(n * out.value)))
+            (ks, kr), (os_, or_) = self._sp_bufs
+            check(self.lib.flite_dit_sp_bind_buffers(self.h, ks.data_ptr(), kr.data_ptr(), os_.data_ptr(),
+                                                     or_.data_ptr()), "flite_dit_sp_bind_buffers")
 
     def set_context(self, ctx_packed: torch.Tensor, cu_host):
         require_gpu(ctx_packed, "context", torch.bfloat16)

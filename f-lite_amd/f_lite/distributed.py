@@ -9,6 +9,11 @@ couple images; sharded APG is per image (documented in DESIGN.md).
 
 Second mode, for single-image latency: CFG-parallel, the uncond and cond branches of the
 same image on two ranks with one all-gather of the branch outputs per step (`cfg_parallel_sample`).
+
+Third mode, single-image latency over any number of GPUs ("ring attention over T"):
+sequence parallelism (`sequence_parallel_sample`). Each rank holds a 1/N slice of the token rows of both CFG
+sequences; the native engine all-gathers the K/V rows once per block (the only data the self-attention needs
+from other ranks) and the output rows once per step, through `all_gather_rows`.
 """
 from __future__ import annotations
 
@@ -135,6 +140,62 @@ def cfg_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Tensor,
         _native.cfg_euler_(x, u, c, guidance_scale, dt)
 
     return cfg_parallel_loop(acc, t_list, dt_list, forward_branch, update, group)
+
+
+def all_gather_rows(send: torch.Tensor, recv: torch.Tensor, group=None) -> None:
+    """recv = cat over the group's ranks (rank order) of `send` (flat device buffers). RCCL all-gather over
+    xGMI with the "nccl" backend; gloo (tests, ranks sharing one GPU) stages through the host."""
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "gloo":
+        host = send.cpu()
+        parts = [torch.empty_like(host) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(parts, host, group=group)
+        recv.copy_(torch.cat(parts))
+    else:
+        dist.all_gather_into_tensor(recv, send, group=group)
+
+
+def sequence_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Tensor,
+                             negative_prompt_embeds: Optional[torch.Tensor] = None, num_inference_steps: int = 30,
+                             guidance_scale: float = 6.0, alpha: Optional[float] = None, group=None) -> torch.Tensor:
+    """Single-image latency mode over the N ranks of `group`: the denoise loop of
+    FLitePipeline.__call__ (pipeline.py:250-297) with every DiT launch split by token rows. Rank r computes rows
+    [r*Tl, (r+1)*Tl) of each sequence of the CFG batch (Tl = ceil(T / N)); per block its K/V rows are
+    all-gathered (2 x T x D bf16 per sequence), per step the output rows. Every rank ends each step with the
+    full model output and applies the same native CFG + Euler update, so all ranks return the same final fp32
+    latents [n_img, 16, h, w]. Weights are replicated. Latents and embeddings are broadcast from the group's
+    first rank first (ranks may have drawn different noise)."""
+    import torch.distributed as dist
+
+    from .pipeline import flow_schedule
+
+    rank, n = dist.get_rank(group), dist.get_world_size(group)
+    eng = dit.engine()
+    dev = dit.device
+    n_img, _, lh, lw = latents.shape
+    pos = prompt_embeds.to(device=dev, dtype=torch.bfloat16).contiguous()
+    do_cfg = guidance_scale >= 1.0
+    neg = torch.zeros_like(pos) if negative_prompt_embeds is None else \
+        negative_prompt_embeds.to(device=dev, dtype=torch.bfloat16).contiguous()  # pipeline.py:160-161
+    if neg.shape != pos.shape or pos.shape[0] != n_img:
+        raise ValueError("prompt / negative embeddings must both be [n_img, L, C_ctx]")
+    lat = latents.to(device=dev, dtype=torch.bfloat16).contiguous()
+    for t in (lat, pos, neg):
+        broadcast_from_group_root(t, group)
+    ctx = torch.cat([neg, pos]) if do_cfg else pos  # uncond first (pipeline.py:266)
+    nseq, L = ctx.shape[0], ctx.shape[1]
+    sched = flow_schedule(num_inference_steps, lh, lw, alpha)
+    acc = lat.float().contiguous()
+    eng.set_sequence_parallel(rank, n, lambda s, r: all_gather_rows(s, r, group))
+    try:
+        eng.prepare(nseq, lh, lw, nseq * L, num_inference_steps, device=dev)
+        eng.set_context(ctx.reshape(nseq * L, -1).contiguous(), [i * L for i in range(nseq + 1)])
+        eng.sample(acc, n_img, [t for t, _ in sched], [dt for _, dt in sched], guidance_scale, do_cfg,
+                   use_graph=False)
+    finally:
+        eng.set_sequence_parallel(0, 1)
+    return acc
 
 
 def max_over_ranks(seconds: float, device=None, group=None) -> float:

@@ -101,6 +101,8 @@ class FLitePipeline:
         self._progress_bar_config = {}
         self._cfg_parallel = False
         self._cfg_group = None
+        self._seq_parallel = False
+        self._sp_group = None
 
     # ---------------------------------------------------------------- loading
     @classmethod
@@ -173,6 +175,21 @@ class FLitePipeline:
 
     def disable_cfg_parallel(self):
         self._cfg_parallel = False
+
+    def enable_sequence_parallel(self, group=None):
+        """Single-image latency over every rank of `group` (no reference counterpart):
+        each rank computes a slice of the token rows of every DiT launch, exchanging K/V rows per block
+        (distributed.sequence_parallel_sample). Every rank calls the pipeline with the same inputs and gets the
+        same images."""
+        import torch.distributed as dist
+
+        if not (dist.is_available() and dist.is_initialized()):
+            raise ValueError("enable_sequence_parallel needs an initialised torch.distributed process group")
+        self._sp_group = group
+        self._seq_parallel = True
+
+    def disable_sequence_parallel(self):
+        self._seq_parallel = False
 
     def enable_model_cpu_offload(self, *a, **k):
         """generate.py:72 (no-op: weights stay resident in the 288 GB HBM)."""
@@ -274,7 +291,14 @@ class FLitePipeline:
         L = prompt_embeds.shape[1]
         if negative_prompt_embeds.shape[1] != L:
             raise ValueError("prompt and negative prompt embeddings must have the same length")
-        if self._cfg_parallel and do_cfg:
+        if self._seq_parallel:
+            if apg_config.enabled:
+                raise NotImplementedError("APG is not available in the sequence-parallel mode")
+            from .distributed import sequence_parallel_sample
+
+            acc = sequence_parallel_sample(dit, latents, prompt_embeds, negative_prompt_embeds, num_inference_steps,
+                                           guidance_scale, alpha, group=self._sp_group)
+        elif self._cfg_parallel and do_cfg:
             if apg_config.enabled:
                 raise NotImplementedError("APG is not available in the CFG-parallel mode")
             from .distributed import cfg_parallel_sample

@@ -245,6 +245,22 @@ int flite_cfg_euler(void* stream, const float* uncond, const float* cond, float*
  */
 int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable);
 
+/* ---- sequence parallelism: one image's rows over `nranks` GPUs ("ring attention over T")
+ * Rank r holds rows [r*Tl, (r+1)*Tl) of every sequence, Tl = ceil(T / nranks) (T = 16 registers + patches;
+ * the last rank's rows past T are padding). Every GEMM, norm and the cross-attention are row-local; the
+ * self-attention of a block needs every key, so after the qkv GEMM each rank's K/V rows are all-gathered and
+ * reordered into whole sequences; after the final projection the output rows are all-gathered, so every rank
+ * ends each forward with the full model output and runs the same CFG/Euler update (flite_dit_sample with
+ * use_graph = 0, or flite_dit_forward + flite_cfg_euler). The exchange is the host's: `fn(user, which,
+ * stream)` must all-gather the caller-bound send buffer of `which` (0 = K/V rows, 1 = output rows) into its
+ * receive buffer (nranks x send bytes, rank order) on `stream` (RCCL all_gather over xGMI; gloo in tests).
+ * Call before flite_dit_prepare; then size (flite_dit_sp_buffer_bytes) and bind the four buffers. bf16 path
+ * only (not with flite_dit_enable_fp8), learned-positional-embedding models excluded. */
+typedef int (*flite_sp_allgather_fn)(void* user, int which, void* stream);
+int flite_dit_set_sequence_parallel(flite_dit* dit, int rank, int nranks, flite_sp_allgather_fn fn, void* user);
+int flite_dit_sp_buffer_bytes(flite_dit* dit, long* kv_send_bytes, long* out_send_bytes);
+int flite_dit_sp_bind_buffers(flite_dit* dit, void* kv_send, void* kv_recv, void* out_send, void* out_recv);
+
 /*
  * 3x3 convolution, padding 1, stride 1 (nn.Conv2d of the diffusers VAE decoder), optionally preceded by a
  * nearest-2x upsample (Upsample2D), as an implicit-GEMM on MFMA. x: NHWC bf16 [h, w, cin] (one image,

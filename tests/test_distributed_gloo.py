@@ -32,6 +32,34 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _rows_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from f_lite.distributed import all_gather_rows
+
+    send = torch.full((5,), rank + 1, dtype=torch.uint8)
+    recv = torch.empty(5 * world, dtype=torch.uint8)
+    all_gather_rows(send, recv)
+    q.put((rank, recv.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_all_gather_rows(world):
+    """The sequence-parallel exchange (distributed.all_gather_rows): rank-ordered concatenation."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(30)
+    want = [r + 1 for r in range(world) for _ in range(5)]
+    assert all(res[r] == want for r in range(world))
+
+
 def _cfg_parallel_worker(rank, world, port, q):
     """One rank of the CFG-parallel loop; the branch forward is the fp32 oracle (test infrastructure)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
