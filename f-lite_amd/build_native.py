@@ -34,6 +34,12 @@ CFLAGS = [
 ]
 
 
+# Per-file extra flags. gemm.hip: no SLP vectorisation -- it packs the fp32 epilogue math (RoPE rotation pairs)
+# into v_pk_*_f32 with op_sel shuffles, which needs extra register pairs and spilled 262 VGPRs in the fused qkv
+# epilogue (packed f32 beside MFMAs is an anti-lever anyway: MI355X guide, per-instruction costs).
+FILE_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"]}
+
+
 def _sources():
     return sorted([p for p in CSRC.iterdir() if p.suffix in (".hip", ".cpp")])
 
@@ -48,7 +54,7 @@ def _compile(src: Path, force: bool) -> Path:
     if not force and obj.exists():
         if obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
             return obj
-    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")

@@ -181,6 +181,8 @@ struct GemmCta {
         if constexpr (GATED_FF) {
           // virtual row wn: sub-tile wn>>4 is gate (even) / up (odd) of output columns (wn>>5)*16 + (wn&15)
           wrow = (long)(wn >> 5) * 16 + (wn & 15);
+        } else if constexpr (EPI == EPI_QKV_NORM_BF16) {
+          if (n0 < p.rope_cols) wrow = rope_perm(wn);  // rotation pairs side by side (qkv_norm_epilogue)
         }
         w_off[i] = (unsigned)((wrow * p.ldw + chunk * 8) * 2);
       }
@@ -380,20 +382,30 @@ struct GemmCta {
     }
   }
 
+  // RoPE heads (q, k): output position j of a head holds original column j/2 (j even) or 128 + j/2 (j odd), so
+  // every rotation pair (c, c + 128) of apply_rotary_emb lands in two adjacent columns of one lane. The W rows
+  // (and bias) are read in that order; q and k share the permutation, so q.k -- all attention uses -- is the
+  // reference's, and v (no RoPE) keeps the original layout.
+  __device__ __forceinline__ static int rope_perm(int n) {
+    const int j = n & 255;
+    return (n & ~255) | (j >> 1) | ((j & 1) << 7);
+  }
+
   // qkv / cross-q epilogue (EPI_QKV_NORM_BF16). A 256-column tile is exactly one head (n0 % 256 == 0). Columns
   // [0, norm_cols) get, in fp32 and with one bf16 rounding at the end: RoPE (apply_rotary_emb, model.py:403-414:
-  // y1 = x1 c + x2 s, y2 = -x1 s + x2 c for the pairs (j, j + 128), tables of the bf16 model) on columns
-  // [0, rope_cols), then QKNorm's RMSNorm over the head (model.py:115-126,180,197). Column j and j + 128 of a row
-  // sit in waves wave_n and wave_n ^ 2 at the same lane and register, so RoPE swaps values through LDS in four
-  // passes of two 16-row blocks (64 KiB); the head's sum of squares is a 4-lane shuffle plus 4 wave partials in LDS.
+  // y1 = x1 c + x2 s, y2 = -x1 s + x2 c for the pairs (c, c + 128), tables of the bf16 model) on columns
+  // [0, rope_cols), then QKNorm's RMSNorm over the head (model.py:115-126,180,197). On RoPE tiles the columns are
+  // in rope_perm order, so each lane rotates its pairs in registers with one 8-B cos and sin load per 4 columns;
+  // the head's sum of squares is a 4-lane shuffle plus 4 wave partials in LDS.
   __device__ __forceinline__ void qkv_norm_epilogue(f32x4 (&acc)[8][4], int m0, int n0, int m_base, int n_base) {
+    const bool rope = n0 < p.rope_cols;  // tile-uniform
     float bias[4][4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n_base + ni * 16 + r;
-        bias[ni][r] = (p.bias != nullptr && n < p.N) ? bf2f(p.bias[n]) : 0.f;
+        bias[ni][r] = (p.bias != nullptr && n < p.N) ? bf2f(p.bias[rope ? rope_perm(n) : n]) : 0.f;
       }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
@@ -403,45 +415,31 @@ struct GemmCta {
         for (int r = 0; r < 4; ++r) acc[mi][ni][r] += bias[ni][r];
     const bool norm = n0 < p.norm_cols;  // tile-uniform
     if (norm) {
-      __syncthreads();  // every wave is done with the k-tile buffers
-      if (n0 < p.rope_cols) {
-        const int pw = wave ^ 2;  // the wave holding the other half of every rotation pair
-        const bool first = wave_n < 2;
-        const int ja = (wave_n & 1) * 64 + lk * 4;  // angle index of (ni = 0, r = 0)
+      if (rope) {
         const int T = (int)p.rope_tokens;
         int tok = min(m_base, p.M - 1) % T;  // token of block mi = 0; + 16 per block (T > 16), wrapped
+        const int jb = n_base & 255;         // head position of (ni = 0, r = 0): even
 #pragma unroll
-        for (int pass = 0; pass < 4; ++pass) {
+        for (int mi = 0; mi < MI; ++mi) {
+          const float* ct = p.rope_cos + (long)tok * 128;
+          const float* st = p.rope_sin + (long)tok * 128;
+          tok = tok + 16 >= T ? tok + 16 - T : tok + 16;  // rows >= M compute garbage and are never stored
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+          for (int ni = 0; ni < 4; ++ni) {
+            const int i0 = (jb + ni * 16) >> 1;  // angle index of the pair in r = 0, 1; r = 2, 3 use i0 + 1
+            const f32x2 c = *(const f32x2*)(ct + i0);
+            const f32x2 sn = *(const f32x2*)(st + i0);
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni)
-              if (2 * pass + i < MI)
-                *(LDS_AS f32x4*)(lds0 + ((wave * 8 + i * 4 + ni) * 64 + lane) * 16) = acc[2 * pass + i][ni];
-          __syncthreads();
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int mi = 2 * pass + i;
-            if (mi >= MI) continue;
-            const float* ct = p.rope_cos + (long)tok * 128 + ja;
-            const float* st = p.rope_sin + (long)tok * 128 + ja;
-            tok = tok + 16 >= T ? tok + 16 - T : tok + 16;  // rows >= M compute garbage and are never stored
-#pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-              const f32x4 other = *(const LDS_AS f32x4*)(lds0 + ((pw * 8 + i * 4 + ni) * 64 + lane) * 16);
-              const f32x4 c = *(const f32x4*)(ct + ni * 16);
-              const f32x4 sn = *(const f32x4*)(st + ni * 16);
-              f32x4 y;
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                y[r] = first ? acc[mi][ni][r] * c[r] + other[r] * sn[r] : -other[r] * sn[r] + acc[mi][ni][r] * c[r];
-              acc[mi][ni] = y;
+            for (int pr = 0; pr < 2; ++pr) {
+              const float x1 = acc[mi][ni][2 * pr], x2 = acc[mi][ni][2 * pr + 1];
+              acc[mi][ni][2 * pr] = x1 * c[pr] + x2 * sn[pr];
+              acc[mi][ni][2 * pr + 1] = -x1 * sn[pr] + x2 * c[pr];
             }
-            __builtin_amdgcn_sched_barrier(0);  // one 16-row block's table loads in flight at a time (registers)
           }
-          __syncthreads();  // the next pass rewrites the exchange area
+          __builtin_amdgcn_sched_barrier(0);  // one 16-row block's table loads in flight at a time (registers)
         }
       }
+      __syncthreads();  // every wave is done with the k-tile buffers (the row partials below reuse LDS)
       // per-head RMSNorm: row sum of squares = 4 lanes (lk) x 4 waves (wave_n)
       const unsigned sums = lds0 + 65536;
 #pragma unroll
@@ -767,7 +765,8 @@ int launch(GemmParams p, hipStream_t s) {
   const int T = (p.M + BM - 1) / BM * num_n;
   p.sk_tiles = choose_sk_tiles(p, T, &p.sk_wgs);
   if (p.conv_in != nullptr) {
-    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true, 8>), dim3(T), dim3(NT), LDS_BYTES, s, p);
+    if constexpr (EPI == EPI_STORE_BF16 || EPI == EPI_STORE_F32)  // gemm_bf16 admits only these with CONV
+      hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true, 8>), dim3(T), dim3(NT), LDS_BYTES, s, p);
   } else if (p.sk_tiles) {
     hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(g_num_cu), dim3(NT), LDS_BYTES, s, p);
   } else if (use_bm224(p)) {
@@ -789,8 +788,10 @@ hipError_t set_attrs() {
   e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, false, 7>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           LDS_BYTES);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             LDS_BYTES);
+  if constexpr (EPI == EPI_STORE_BF16 || EPI == EPI_STORE_F32)
+    return hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, true, 8>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+  return hipSuccess;
 }
 
 }  // namespace

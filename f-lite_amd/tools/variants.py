@@ -36,14 +36,16 @@ def build(src, name, args):
     out = HERE / "variants" / name
     out.mkdir(parents=True, exist_ok=True)
     defines, subs = [], []
+    text = (bn.CSRC / f"{src}.hip").read_text()
     it = iter(args)
     for a in it:
         if a == "--sub":
             old, new = next(it).split("==>")
             subs.append((old, new))
+        elif a == "--from":  # another version of the source (e.g. `git show HEAD~1:...` saved to a file)
+            text = Path(next(it)).read_text()
         else:
             defines.append(a)
-    text = (bn.CSRC / f"{src}.hip").read_text()
     for old, new in subs:
         if old not in text:
             raise SystemExit(f"substitution target not found: {old!r}")
@@ -51,7 +53,7 @@ def build(src, name, args):
     tmp = out / f"{src}.hip"
     tmp.write_text(text)
     obj = out / f"{src}.o"
-    cmd = [bn.HIPCC, *bn.CFLAGS, *defines, "-c", str(tmp), "-o", str(obj)]
+    cmd = [bn.HIPCC, *bn.CFLAGS, *bn.FILE_FLAGS.get(f"{src}.hip", []), *defines, "-c", str(tmp), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(r.stderr[-4000:])
@@ -100,13 +102,45 @@ def time_gemms(iters=20):
     return res
 
 
+def time_attn(iters=30):
+    import torch
+    from f_lite import _native as nat
+
+    torch.manual_seed(0)
+    res = {}
+    B, H, D = 2, 12, 256
+    for name, T, Lk in (("self", 4112, 4112), ("cross", 4112, 512), ("cross_notail", 4096, 512)):
+        q = torch.nn.functional.normalize(torch.randn(B * T, H, D, device="cuda"), dim=-1).mul(16).bfloat16()
+        k = torch.nn.functional.normalize(torch.randn(B * Lk, H, D, device="cuda"), dim=-1).mul(16).bfloat16()
+        v = torch.randn(B * Lk, H, D, device="cuda").bfloat16()
+        cu_q = torch.tensor([0, T, 2 * T], dtype=torch.int32, device="cuda")
+        cu_k = torch.tensor([0, Lk, 2 * Lk], dtype=torch.int32, device="cuda")
+        out = torch.empty_like(q)
+        ws = nat.attn_workspace("cuda", B, H)
+        run = lambda: nat.attn_varlen(q, k, v, cu_q, cu_k, T, D ** -0.5, out=out, max_score=16.5,  # noqa: E731
+                                      workspace=ws, max_k=Lk)
+        for _ in range(3):
+            run()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(iters):
+            run()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / iters
+        res[name] = (ms, 4.0 * B * H * T * Lk * D / ms / 1e9)
+    return res
+
+
 def main():
     mode, src = sys.argv[1], sys.argv[2]
     if mode == "build":
         build(src, sys.argv[3], sys.argv[4:])
         return
     if mode == "child":
-        print("RESULT " + json.dumps(time_gemms()), flush=True)
+        print("RESULT " + json.dumps(time_attn() if src == "attention" else time_gemms()), flush=True)
         return
     args = sys.argv[3:]
     rounds = 3
