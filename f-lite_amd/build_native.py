@@ -37,7 +37,7 @@ CFLAGS = [
 # Per-file extra flags. gemm.hip: no SLP vectorisation -- it packs the fp32 epilogue math (RoPE rotation pairs)
 # into v_pk_*_f32 with op_sel shuffles, which needs extra register pairs and spilled 262 VGPRs in the fused qkv
 # epilogue (packed f32 beside MFMAs is an anti-lever anyway: MI355X guide, per-instruction costs).
-FILE_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"], "gemm_fp8.hip": ["-fno-slp-vectorize"]}
 
 
 def _sources():

@@ -47,6 +47,89 @@ __device__ __forceinline__ float gelu_tanh_f(float x) {
   return 0.5f * x * (1.0f + t);
 }
 
+// Column order of the RoPE heads (q, k) written by the fused qkv GEMM epilogues: output position j of a 256-wide
+// head holds original column j/2 (j even) or 128 + j/2 (j odd), so each rotation pair (c, c + 128) of
+// apply_rotary_emb lands in two adjacent columns of one lane. q and k share it, so q.k is unchanged.
+__host__ __device__ __forceinline__ int rope_perm(int n) {
+  const int j = n & 255;
+  return (n & ~255) | (j >> 1) | ((j & 1) << 7);
+}
+
+// Factorised 2-D RoPE table read by the fused qkv GEMM epilogues (rope_axes_table, elementwise.hip). TwoDimRotary
+// (model.py:334-386) gives token t = reg + y*w + x the angles cat(y * inv_freq, x * inv_freq) (64 each) and the
+// registers angle 0, so the [T][128] cos / sin tables of rope_table hold only 1 + h + w distinct 64-angle rows:
+// row 0 = registers (cos 1, sin 0), row 1 + y = the y axis, row 1 + h + x = the x axis, each [64][2] fp32 with cos
+// and sin interleaved. Same values in (1 + h + w) rows instead of T: 72 KB at 1344x896, L2-resident.
+struct RopeAxes {
+  const float* cs = nullptr;  // [1 + h + w][64][2]
+  int tokens = 0;             // rows per sequence in the launch: row m is local token m % tokens
+  int tok0 = 0;               // global token of local token 0 (sequence parallelism: rank * tokens)
+  int reg = 0, h = 0, w = 0;
+  float inv_w = 0.f;          // 1 / w
+
+  // table row of global token g for angles [0, 64) (axis_mask 0) or [64, 128) (axis_mask -1); tokens past the sequence
+  // (padding rows of the last sequence-parallel rank) clamp to its last row
+  // (branch-free: a select here had become per-block control flow that kept every block's loads in flight)
+  __device__ __forceinline__ int row(int g, int axis_mask) const {
+    const int q = max(g - reg, 0);
+    int y = (int)((float)q * inv_w);
+    int x = q - y * w;
+    const int lo = x >> 31;  // x < 0: one row too far
+    y += lo;
+    x += lo & w;
+    const int hi = (w - 1 - x) >> 31;  // x >= w: one row short
+    y -= hi;
+    x -= hi & w;
+    y = min(y, h - 1);
+    const int r = 1 + ((y & ~axis_mask) | ((h + x) & axis_mask));
+    return r & ((reg - 1 - g) >> 31);  // registers (g < reg): row 0
+  }
+};
+
+// RoPE (apply_rotary_emb, model.py:403-414: y1 = x1 c + x2 s, y2 = -x1 s + x2 c) of one wave's GEMM accumulators
+// in the gemm.hip / gemm_fp8.hip layout: the lane holds C[m][n .. n+3], m = m_base + mi*16, n = n0 + wave_n*64 +
+// lk*4 + ni*16, columns in rope_perm order, so (r 0, 1) and (r 2, 3) are rotation pairs with angles i0 and i0 + 1,
+// i0 = wave_n*32 + lk*2 + ni*8: waves 0-1 take the y axis, 2-3 the x axis. The table is small enough to stay
+// L2-resident. Rows >= M rotate garbage and are never stored.
+template <int MI>
+__device__ __forceinline__ void rope_rotate(f32x4 (&acc)[8][4], const RopeAxes& ra, int m_base, int M, int wave_n,
+                                            int lk) {
+  const int axis_mask = wave_n >= 2 ? -1 : 0;
+  const float* base = ra.cs + ((wave_n & 1) * 32 + lk * 2) * 2;
+  const int T = ra.tokens;
+  const int step = 16 % T;  // next block's token (sequences may be shorter than 16 rows)
+  int tok = min(m_base, M - 1) % T;
+  auto fetch = [&](int t, f32x4(&d)[4]) {
+    const float* b = base + (long)ra.row(ra.tok0 + t, axis_mask) * 128;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) d[ni] = *(const f32x4*)(b + ni * 16);
+  };
+  f32x4 cur[4], nxt[4];
+  fetch(tok, cur);
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi) {
+    if (mi + 1 < MI) {
+      tok += step;
+      if (tok >= T) tok -= T;
+      fetch(tok, nxt);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const float c = cur[ni][2 * pr], sn = cur[ni][2 * pr + 1];
+        const float x1 = acc[mi][ni][2 * pr], x2 = acc[mi][ni][2 * pr + 1];
+        acc[mi][ni][2 * pr] = x1 * c + x2 * sn;
+        acc[mi][ni][2 * pr + 1] = -x1 * sn + x2 * c;
+      }
+    __builtin_amdgcn_sched_barrier(0);  // at most two 16-row blocks' table loads in flight (registers)
+    if (mi + 1 < MI) {
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) cur[ni] = nxt[ni];
+    }
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -75,6 +75,19 @@ void DitEngine::free_ws() {
   x_ = nullptr;
   kv_full_ = nullptr;
   cu_full_ = nullptr;
+  rope_axes_ = nullptr;
+}
+
+RopeAxes DitEngine::rope_axes() const {
+  RopeAxes r;
+  r.cs = rope_axes_;
+  r.tokens = Tl_;
+  r.tok0 = sp_rank_ * Tl_;  // the rows held here start at this token of the sequence
+  r.reg = R;
+  r.h = Hl_ / P;
+  r.w = Wl_ / P;
+  r.inv_w = 1.f / (float)r.w;
+  return r;
 }
 
 void DitEngine::free_fp8_weights() {
@@ -253,6 +266,7 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
     FLITE_HIP_CHECK(hipMemcpy(cu_full_, cuf.data(), (B + 1) * 4, hipMemcpyHostToDevice));
   }
   if (alloc((void**)&inv_freq_, 64 * 4)) return 1;
+  if (alloc((void**)&rope_axes_, (long)(1 + Hl / P + Wl / P) * 128 * 4)) return 1;
   if (alloc((void**)&ctx_p_, (long)std::max(n_ctx_max, 1) * D * 2)) return 1;
   ctx_kv_.assign(cfg.depth, nullptr);
   for (int i = 0; i < cfg.depth; ++i)
@@ -277,6 +291,7 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   for (int i = 0; i < 64; ++i) inv[i] = (float)(1.0 / pow((double)cfg.rope_base, (double)(2 * i) / (double)rdim));
   FLITE_HIP_CHECK(hipMemcpy(inv_freq_, inv, sizeof(inv), hipMemcpyHostToDevice));
   if (rope_table(inv_freq_, cos_, sin_, Hl / P, Wl / P, R, cfg.bf16_rope_tables, 0)) return 1;
+  if (rope_axes_table(inv_freq_, rope_axes_, Hl / P, Wl / P, cfg.bf16_rope_tables, 0)) return 1;
   if (fp8_ && alloc_fp8_act()) return 1;
   FLITE_HIP_CHECK(hipDeviceSynchronize());
   nctx_ = 0;
@@ -473,9 +488,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.N = 3 * D;
     g.K = D;
     // RoPE + QK-norm of the q and k heads ("(k h d)" layout, model.py:163) in the GEMM epilogue
-    g.rope_cos = cos_ + rope_off;
-    g.rope_sin = sin_ + rope_off;
-    g.rope_tokens = Tl_;
+    g.rope = rope_axes();
     g.norm_cols = 2 * D;
     g.rope_cols = cfg.use_rope ? 2 * D : 0;
     if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
@@ -634,12 +647,15 @@ int DitEngine::enable_fp8(hipStream_t s, bool on) {
       if (buf(d, (size_t)rows * K) || buf(sc, (size_t)(K / 128) * rows * 4)) return 1;
       return quant_rows_fp8(w, K, rows, K, *d, K, *sc, rows, s);
     };
+    // fused RoPE epilogue: the q/k rows of the qkv weight in rope_perm order (gemm_fp8 EPI8_QKV_NORM_BF16)
+    const long perm_rows = (fuse_qk_norm() && cfg.use_rope) ? 2L * D : 0;
     for (int i = 0; i < cfg.depth; ++i) {
       const BlockW& b = w_.blocks[i];
       Fp8W& f = w8_[i];
-      if (q(b.qkv_w, 3L * D, D, &f.qkv, &f.qkv_s) || q(b.proj_w, D, D, &f.proj, &f.proj_s) ||
-          q(b.down_w, D, F, &f.down, &f.down_s))
+      if (buf(&f.qkv, (size_t)3 * D * D) || buf(&f.qkv_s, (size_t)(D / 128) * 3 * D * 4) ||
+          quant_rows_fp8_perm(b.qkv_w, D, 3L * D, D, f.qkv, D, f.qkv_s, 3L * D, perm_rows, s))
         return 1;
+      if (q(b.proj_w, D, D, &f.proj, &f.proj_s) || q(b.down_w, D, F, &f.down, &f.down_s)) return 1;
       if (b.cross && (q(b.cq_w, D, D, &f.cq, &f.cq_s) || q(b.cproj_w, D, D, &f.cproj, &f.cproj_s))) return 1;
       if (buf(&f.gu, (size_t)2 * F * D) || buf(&f.gu_s, (size_t)(D / 128) * 2 * F * 4)) return 1;
       if (quant_gateup_fp8(b.gate_w, b.up_w, D, F, D, f.gu, f.gu_s, s)) return 1;
@@ -678,7 +694,8 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     return rmsnorm_mod(nm, false, s);
   };
   auto g8 = [&](const uint8_t* A, const uint8_t* As, const uint8_t* W, const uint8_t* Ws, long w_rows, int N, int K,
-                const bf16_t* bias, int epi, void* out, long ldo, const float* gate) -> int {
+                const bf16_t* bias, int epi, void* out, long ldo, const float* gate, int norm_cols = 0,
+                int rope_cols = 0) -> int {
     GemmFp8Params g;
     g.A = A;
     g.lda = K;
@@ -700,6 +717,11 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     if (epi == EPI8_SWIGLU_FP8) {
       g.out_sc = hbuf8_s_;
       g.out_rows_pad = mpad_;
+    }
+    if (epi == EPI8_QKV_NORM_BF16) {
+      g.norm_cols = norm_cols;
+      g.rope_cols = rope_cols;
+      g.rope = rope_axes();
     }
     return gemm_fp8(g, epi, s);
   };
@@ -744,10 +766,12 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   // --- self attention ---
   if (norm8(b.norm1, shift_sa, scale_sa)) return 1;
   if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
-  if (g8(nbuf8_, nbuf8_s_, q.qkv, q.qkv_s, 3L * D, 3 * D, D, b.qkv_b, EPI8_STORE_BF16, qkv_, 3L * D, nullptr))
+  const bool fused = fuse_qk_norm();  // RoPE + QK-norm in the GEMM epilogue (the weights were quantised to match)
+  if (g8(nbuf8_, nbuf8_s_, q.qkv, q.qkv_s, 3L * D, 3 * D, D, b.qkv_b, fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16,
+         qkv_, 3L * D, nullptr, 2 * D, cfg.use_rope ? 2 * D : 0))
     return 1;
   if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
-  if (qk_norm(3L * D, 2 * H, cfg.use_rope ? 2 * H : 0)) return 1;
+  if (!fused && qk_norm(3L * D, 2 * H, cfg.use_rope ? 2 * H : 0)) return 1;
   if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
   if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, Tl_)) return 1;
   if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
@@ -756,8 +780,10 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   // --- cross attention ---
   if (b.cross) {
     if (norm8(b.norm2, shift_ca, scale_ca)) return 1;
-    if (g8(nbuf8_, nbuf8_s_, q.cq, q.cq_s, D, D, D, b.cq_b, EPI8_STORE_BF16, qkv_, D, nullptr)) return 1;
-    if (qk_norm(D, H, 0)) return 1;
+    if (g8(nbuf8_, nbuf8_s_, q.cq, q.cq_s, D, D, D, b.cq_b, fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16, qkv_, D,
+           nullptr, D, 0))
+      return 1;
+    if (!fused && qk_norm(D, H, 0)) return 1;
     if (attn(qkv_, D, ctx_kv_[blk], ctx_kv_[blk] + D, 2L * D, cu_ctx_, ctx_max_len_)) return 1;
     if (quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
     if (g8(obuf8_, obuf8_s_, q.cproj, q.cproj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_ca)) return 1;

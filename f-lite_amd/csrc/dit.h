@@ -108,6 +108,8 @@ class DitEngine {
   long attn_ws_bytes_ = 0;
   int *cu_self_ = nullptr, *cu_ctx_ = nullptr;
   float *cos_ = nullptr, *sin_ = nullptr, *inv_freq_ = nullptr;
+  float* rope_axes_ = nullptr;  // factorised table of the fused qkv epilogues (common.h RopeAxes)
+  RopeAxes rope_axes() const;
   bf16_t* ctx_p_ = nullptr;
   std::vector<bf16_t*> ctx_kv_;  // per block (cross blocks only)
   float* tdev_ = nullptr;

@@ -629,6 +629,37 @@ int timestep_embed(const float* t, bf16_t* emb, int n, int D, int quantize, hipS
   return 0;
 }
 
+// [1 + hh + ww][64][2]: row 0 = (1, 0), rows 1 + y and 1 + hh + x = (cos, sin) of pos * inv_freq, rounded as
+// rope_table does (RopeAxes, common.h)
+__global__ __launch_bounds__(256) void rope_axes_kernel(const float* inv_freq, float* cs, int hh, int ww,
+                                                        int round_bf16) {
+  const int total = (1 + hh + ww) * 64;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int row = idx / 64, j = idx % 64;
+    float c = 1.f, s = 0.f;
+    if (row > 0) {
+      const float pos = (float)(row <= hh ? row - 1 : row - 1 - hh);
+      const float a = pos * inv_freq[j];
+      c = cosf(a);
+      s = sinf(a);
+      if (round_bf16) {
+        c = bf2f(f2bf(c));
+        s = bf2f(f2bf(s));
+      }
+    }
+    cs[2 * idx] = c;
+    cs[2 * idx + 1] = s;
+  }
+}
+
+int rope_axes_table(const float* inv_freq, float* cs, int hh, int ww, int round_bf16, hipStream_t s) {
+  FLITE_REQUIRE(hh > 0 && ww > 0, "rope_axes_table: empty grid");
+  hipLaunchKernelGGL(rope_axes_kernel, dim3((unsigned)(((1 + hh + ww) * 64 + 255) / 256)), dim3(256), 0, s, inv_freq,
+                     cs, hh, ww, round_bf16);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
 int rope_table(const float* inv_freq, float* cos_t, float* sin_t, int hh, int ww, int R, int round_bf16,
                hipStream_t s) {
   const long total = (long)(R + hh * ww) * 128;

@@ -31,6 +31,7 @@ enum GemmFp8Epilogue {
   EPI8_RESID_F32 = 2,   // out_f32[m][n] += gate[seg(m)][n] * (acc + bias[n])
   EPI8_SWIGLU_FP8 = 4,  // W8 = gate|up interleaved in 16-row sub-tiles (N = 2F): out8[m][f] = MX(silu(g) * u),
                         // scales to out_sc [F/128][out_rows_pad][4]
+  EPI8_QKV_NORM_BF16 = 5,  // engine-internal: bf16 store with RoPE + QK-norm of columns [0, norm_cols) (gemm.hip)
 };
 
 struct GemmFp8Params {
@@ -51,11 +52,19 @@ struct GemmFp8Params {
   long gate_seg_stride = 0;
   int rows_per_seg = 1;
   int M = 0, N = 0, K = 0;
+  // EPI8_QKV_NORM_BF16 (as gemm.hip's EPI_QKV_NORM_BF16): factorised RoPE table (common.h RopeAxes); columns
+  // [0, rope_cols) are q/k heads whose W rows were quantised in rope_perm order (quant_rows_fp8_perm)
+  RopeAxes rope;
+  int rope_cols = 0, norm_cols = 0;
+  float norm_eps = 1e-6f;
 };
 
 int gemm_fp8(const GemmFp8Params& p, int epi, hipStream_t s);
 int quant_rows_fp8(const bf16_t* src, long ld_src, long rows, int K, uint8_t* dst, long ld_dst, uint8_t* scales,
                    long rows_pad, hipStream_t s);
+// quant_rows_fp8 with destination row v < perm_rows taken from source row rope_perm(v) (the fused fp8 qkv epilogue)
+int quant_rows_fp8_perm(const bf16_t* src, long ld_src, long rows, int K, uint8_t* dst, long ld_dst, uint8_t* scales,
+                        long rows_pad, long perm_rows, hipStream_t s);
 int quant_gateup_fp8(const bf16_t* gate, const bf16_t* up, long ld_src, int F, int K, uint8_t* dst, uint8_t* scales,
                      hipStream_t s);
 

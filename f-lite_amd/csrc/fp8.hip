@@ -19,9 +19,11 @@ namespace {
 // 32 consecutive elements of one row per thread: 4 x 16-B loads, 2 x 16-B stores, one scale byte.
 // INTERLEAVE (SwiGLU gate/up weights): destination row v is row (v >> 5) * 16 + (v & 15) of src (16-row sub-tile
 // v >> 4 even) or src2 (odd) -- the gate|up sub-tile order the GEMM's SwiGLU epilogue pairs up.
-template <bool INTERLEAVE>
+// PERM (fused qkv epilogue): destination row v < perm_rows is source row rope_perm(v).
+template <bool INTERLEAVE, bool PERM = false>
 __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* src, const bf16_t* src2, long lds, long rows,
-                                                         int K, uint8_t* dst, long ldd, uint8_t* sc, long rows_pad) {
+                                                         int K, uint8_t* dst, long ldd, uint8_t* sc, long rows_pad,
+                                                         long perm_rows = 0) {
   const long nblk = (long)K / 32;
   const long total = rows * nblk;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -32,6 +34,9 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* src, cons
     if constexpr (INTERLEAVE) {
       s = ((v >> 4) & 1) ? src2 : src;
       r = (v >> 5) * 16 + (v & 15);
+    }
+    if constexpr (PERM) {
+      if (v < perm_rows) r = rope_perm((int)v);
     }
     const u32x4* p = (const u32x4*)(s + r * lds + b * 32);
     float x[32];
@@ -79,6 +84,17 @@ int quant_rows_fp8(const bf16_t* src, long ld_src, long rows, int K, uint8_t* ds
   FLITE_REQUIRE(rows_pad >= rows, "quant_fp8: rows_pad < rows");
   hipLaunchKernelGGL(quant_rows_kernel<false>, dim3(grid_for(rows * (K / 32))), dim3(256), 0, s, src, src, ld_src,
                      rows, K, dst, ld_dst, scales, rows_pad);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int quant_rows_fp8_perm(const bf16_t* src, long ld_src, long rows, int K, uint8_t* dst, long ld_dst, uint8_t* scales,
+                        long rows_pad, long perm_rows, hipStream_t s) {
+  FLITE_REQUIRE(K % 128 == 0, "quant_fp8: K must be a multiple of 128");
+  FLITE_REQUIRE(ld_src % 8 == 0 && ld_dst % 16 == 0, "quant_fp8: row strides must keep 16-B alignment");
+  FLITE_REQUIRE(rows_pad >= rows && perm_rows % 256 == 0 && perm_rows <= rows, "quant_fp8_perm: bad row counts");
+  hipLaunchKernelGGL((quant_rows_kernel<false, true>), dim3(grid_for(rows * (K / 32))), dim3(256), 0, s, src, src,
+                     ld_src, rows, K, dst, ld_dst, scales, rows_pad, perm_rows);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

@@ -382,21 +382,17 @@ struct GemmCta {
     }
   }
 
-  // RoPE heads (q, k): output position j of a head holds original column j/2 (j even) or 128 + j/2 (j odd), so
-  // every rotation pair (c, c + 128) of apply_rotary_emb lands in two adjacent columns of one lane. The W rows
-  // (and bias) are read in that order; q and k share the permutation, so q.k -- all attention uses -- is the
-  // reference's, and v (no RoPE) keeps the original layout.
-  __device__ __forceinline__ static int rope_perm(int n) {
-    const int j = n & 255;
-    return (n & ~255) | (j >> 1) | ((j & 1) << 7);
-  }
+  // RoPE heads (q, k): the W rows (and bias) are read in rope_perm order (common.h), so every rotation pair of
+  // apply_rotary_emb sits in two adjacent columns of one lane; v (no RoPE) keeps the original layout.
 
   // qkv / cross-q epilogue (EPI_QKV_NORM_BF16). A 256-column tile is exactly one head (n0 % 256 == 0). Columns
   // [0, norm_cols) get, in fp32 and with one bf16 rounding at the end: RoPE (apply_rotary_emb, model.py:403-414:
   // y1 = x1 c + x2 s, y2 = -x1 s + x2 c for the pairs (c, c + 128), tables of the bf16 model) on columns
   // [0, rope_cols), then QKNorm's RMSNorm over the head (model.py:115-126,180,197). On RoPE tiles the columns are
-  // in rope_perm order, so each lane rotates its pairs in registers with one 8-B cos and sin load per 4 columns;
-  // the head's sum of squares is a 4-lane shuffle plus 4 wave partials in LDS.
+  // in rope_perm order, so each lane rotates its pairs in registers; the angles of those pairs belong to one axis
+  // per wave (waves 0-1: y, 2-3: x) and come from the factorised table (RopeAxes) as one 16-B (cos, sin, cos, sin)
+  // load per 4 columns, fetched one 16-row block ahead. The head's sum of squares is a 4-lane shuffle plus 4 wave
+  // partials in LDS.
   __device__ __forceinline__ void qkv_norm_epilogue(f32x4 (&acc)[8][4], int m0, int n0, int m_base, int n_base) {
     const bool rope = n0 < p.rope_cols;  // tile-uniform
     float bias[4][4];
@@ -415,30 +411,7 @@ struct GemmCta {
         for (int r = 0; r < 4; ++r) acc[mi][ni][r] += bias[ni][r];
     const bool norm = n0 < p.norm_cols;  // tile-uniform
     if (norm) {
-      if (rope) {
-        const int T = (int)p.rope_tokens;
-        int tok = min(m_base, p.M - 1) % T;  // token of block mi = 0; + 16 per block (T > 16), wrapped
-        const int jb = n_base & 255;         // head position of (ni = 0, r = 0): even
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) {
-          const float* ct = p.rope_cos + (long)tok * 128;
-          const float* st = p.rope_sin + (long)tok * 128;
-          tok = tok + 16 >= T ? tok + 16 - T : tok + 16;  // rows >= M compute garbage and are never stored
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            const int i0 = (jb + ni * 16) >> 1;  // angle index of the pair in r = 0, 1; r = 2, 3 use i0 + 1
-            const f32x2 c = *(const f32x2*)(ct + i0);
-            const f32x2 sn = *(const f32x2*)(st + i0);
-#pragma unroll
-            for (int pr = 0; pr < 2; ++pr) {
-              const float x1 = acc[mi][ni][2 * pr], x2 = acc[mi][ni][2 * pr + 1];
-              acc[mi][ni][2 * pr] = x1 * c[pr] + x2 * sn[pr];
-              acc[mi][ni][2 * pr + 1] = -x1 * sn[pr] + x2 * c[pr];
-            }
-          }
-          __builtin_amdgcn_sched_barrier(0);  // one 16-row block's table loads in flight at a time (registers)
-        }
-      }
+      if (rope) rope_rotate<MI>(acc, p.rope, m_base, p.M, wave_n, lk);
       __syncthreads();  // every wave is done with the k-tile buffers (the row partials below reuse LDS)
       // per-head RMSNorm: row sum of squares = 4 lanes (lk) x 4 waves (wave_n)
       const unsigned sums = lds0 + 65536;
@@ -867,7 +840,7 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
       FLITE_REQUIRE(p.N % 256 == 0 && p.ldo % 4 == 0 && p.norm_cols % 256 == 0 && p.rope_cols % 256 == 0 &&
                         p.rope_cols <= p.norm_cols && p.norm_cols <= p.N,
                     "gemm(qkv_norm): heads of 256 columns (N, norm_cols, rope_cols multiples of 256)");
-      FLITE_REQUIRE(p.rope_cols == 0 || (p.rope_cos && p.rope_sin && p.rope_tokens > 0),
+      FLITE_REQUIRE(p.rope_cols == 0 || (p.rope.cs && p.rope.tokens > 0 && p.rope.h > 0 && p.rope.w > 0),
                     "gemm(qkv_norm): RoPE tables missing");
       FLITE_REQUIRE(p.out_seg == 0 && p.act == 0 && p.resid == nullptr, "gemm(qkv_norm): plain row layout only");
       launch<EPI_QKV_NORM_BF16>(p, stream);

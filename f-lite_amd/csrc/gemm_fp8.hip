@@ -303,8 +303,64 @@ struct Fp8Cta {
     if (kt < nk) ktile<0>(acc, wf, ws, a0, s0, a1, s1, kt);
   }
 
+  // RoPE + QK-norm, as gemm.hip's qkv_norm_epilogue: RoPE tiles (n0 < rope_cols) hold the q/k heads in rope_perm
+  // column order (the fp8 weight rows were quantised in that order), so each lane rotates its pairs in registers;
+  // the per-head RMSNorm sums squares over 4 lanes and the 4 wave_n waves (LDS partials); one bf16 rounding.
+  __device__ __forceinline__ void qkv_norm_epilogue(f32x4 (&acc)[8][4], int n0, int m_base, int n_base) {
+    const bool rope = n0 < p.rope_cols;  // tile-uniform
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n_base + ni * 16 + r;
+        const float b = (p.bias != nullptr && n < p.N) ? bf2f(p.bias[rope ? rope_perm(n) : n]) : 0.f;
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) acc[mi][ni][r] += b;
+      }
+    if (n0 < p.norm_cols) {
+      if (rope) rope_rotate<MI>(acc, p.rope, m_base, p.M, wave_n, lk);
+      __syncthreads();  // every wave is done with the k-tile buffers
+      const unsigned sums = lds0 + 65536;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        float ss = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ss += acc[mi][ni][r] * acc[mi][ni][r];
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        if (lk == 0) *(LDS_AS float*)(sums + (((wave_m * 8 + mi) * 16 + lr) * 4 + wave_n) * 4) = ss;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const f32x4 part = *(const LDS_AS f32x4*)(sums + ((wave_m * 8 + mi) * 16 + lr) * 16);
+        const float rn = rsqrtf((part[0] + part[1] + part[2] + part[3]) * (1.f / 256.f) + p.norm_eps);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[mi][ni][r] *= rn;
+      }
+    }
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m = m_base + mi * 16;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int n = n_base + ni * 16;
+        if (n >= p.N) continue;
+        u32x2 w;
+        w.x = pack2bf(acc[mi][ni][0], acc[mi][ni][1]);
+        w.y = pack2bf(acc[mi][ni][2], acc[mi][ni][3]);
+        *(u32x2*)((bf16_t*)p.out + (long)m * p.ldo + n) = w;
+      }
+    }
+  }
+
   // ---- epilogues: lane holds C[m][n..n+3], m = m_base + mi*16, n = n_base + ni*16 (gemm.hip layout) ----
-  __device__ __forceinline__ void epilogue(const f32x4 (&acc)[8][4], int m0, int n0) {
+  __device__ __forceinline__ void epilogue(f32x4 (&acc)[8][4], int m0, int n0) {
     const int m_base = m0 + wave_m * WM + lr;
     const int n_base = n0 + wave_n * 64 + lk * 4;
     if constexpr (EPI == EPI8_SWIGLU_FP8) {
@@ -377,6 +433,9 @@ struct Fp8Cta {
             if (mok[i] && nok[ni]) *(f32x4*)(orow[i] + nc[ni]) = x;
           }
       }
+      return;
+    } else if constexpr (EPI == EPI8_QKV_NORM_BF16) {
+      qkv_norm_epilogue(acc, n0, m_base, n_base);
       return;
     } else {  // EPI8_STORE_BF16
       float bias[4][4];
@@ -455,6 +514,7 @@ int init8() {
   FLITE_HIP_CHECK(set_attrs8<EPI8_STORE_BF16>());
   FLITE_HIP_CHECK(set_attrs8<EPI8_RESID_F32>());
   FLITE_HIP_CHECK(set_attrs8<EPI8_SWIGLU_FP8>());
+  FLITE_HIP_CHECK(set_attrs8<EPI8_QKV_NORM_BF16>());
   int dev = 0;
   FLITE_HIP_CHECK(hipGetDevice(&dev));
   FLITE_HIP_CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -512,6 +572,14 @@ int gemm_fp8(const GemmFp8Params& p, int epi, hipStream_t s) {
                     "gemm_fp8(swiglu): output scales / stride");
       FLITE_REQUIRE(p.bias == nullptr, "gemm_fp8(swiglu): no bias");
       launch8<EPI8_SWIGLU_FP8>(p, s);
+      break;
+    case EPI8_QKV_NORM_BF16:
+      FLITE_REQUIRE(p.N % 256 == 0 && p.ldo % 4 == 0 && p.norm_cols % 256 == 0 && p.rope_cols % 256 == 0 &&
+                        p.rope_cols <= p.norm_cols && p.norm_cols <= p.N,
+                    "gemm_fp8(qkv_norm): heads of 256 columns");
+      FLITE_REQUIRE(p.rope_cols == 0 || (p.rope.cs && p.rope.tokens > 0 && p.rope.h > 0 && p.rope.w > 0),
+                    "gemm_fp8(qkv_norm): RoPE tables missing");
+      launch8<EPI8_QKV_NORM_BF16>(p, s);
       break;
     default:
       FLITE_REQUIRE(false, "gemm_fp8: unknown epilogue");

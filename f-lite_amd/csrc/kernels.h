@@ -42,10 +42,8 @@ struct GemmParams {
   int* sk_flags = nullptr;
   int sk_tiles = 0;  // set by the launcher
   int sk_wgs = 0;    // set by the launcher: workgroups sharing the stream-K iterations
-  // EPI_QKV_NORM_BF16: RoPE tables fp32 [rope_tokens, 128] (row m uses table row m % rope_tokens)
-  const float* rope_cos = nullptr;
-  const float* rope_sin = nullptr;
-  long rope_tokens = 0;
+  // EPI_QKV_NORM_BF16: factorised RoPE table (common.h RopeAxes) for columns [0, rope_cols)
+  RopeAxes rope;
   int rope_cols = 0, norm_cols = 0;
   float norm_eps = 1e-6f;
 };
@@ -137,6 +135,8 @@ int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, 
 int timestep_embed(const float* t, bf16_t* emb, int n, int D, int quantize, hipStream_t s);
 int rope_table(const float* inv_freq, float* cos_t, float* sin_t, int hh, int ww, int R, int round_bf16,
                hipStream_t s);
+// the same angles as rope_table, factorised per axis (common.h RopeAxes): cs [1 + hh + ww][64][2]
+int rope_axes_table(const float* inv_freq, float* cs, int hh, int ww, int round_bf16, hipStream_t s);
 int gather_rows(const bf16_t* src, bf16_t* dst, const int* idx, long n, int cols, hipStream_t s);
 
 }  // namespace flite

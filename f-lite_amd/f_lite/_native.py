@@ -470,12 +470,20 @@ class DitEngine:
         check(self.lib.flite_dit_set_timesteps(self.h, stream_ptr(t.device), t.data_ptr(), t.numel(), int(quantize)),
               "flite_dit_set_timesteps")
 
+    def _check_sp(self, status, what):
+        """check(), re-raising the exception of a failed sequence-parallel exchange callback if there was one."""
+        err, self._sp_error = self._sp_error, None
+        if status != 0 and err is not None:
+            raise FliteError(f"{what}: sequence-parallel exchange failed: {err!r}") from err
+        check(status, what)
+
     def forward(self, x: torch.Tensor, out: torch.Tensor, t_row0=0, t_row_step=1):
         require_gpu(x, "x")
         require_gpu(out, "out")
-        check(self.lib.flite_dit_forward(self.h, stream_ptr(x.device), x.data_ptr(), int(x.dtype == torch.bfloat16),
-                                         x.shape[0], t_row0, t_row_step, out.data_ptr(),
-                                         int(out.dtype == torch.bfloat16)), "flite_dit_forward")
+        self._check_sp(self.lib.flite_dit_forward(self.h, stream_ptr(x.device), x.data_ptr(),
+                                                  int(x.dtype == torch.bfloat16), x.shape[0], t_row0, t_row_step,
+                                                  out.data_ptr(), int(out.dtype == torch.bfloat16)),
+                       "flite_dit_forward")
         return out
 
     def enable_fp8(self, on: bool = True, device=None):
@@ -496,9 +504,9 @@ class DitEngine:
         n = len(t_list)
         ta = (_f * n)(*t_list)
         da = (_f * n)(*dt_list)
-        check(self.lib.flite_dit_sample(self.h, stream_ptr(acc.device), acc.data_ptr(), n_img, n, ta, da,
-                                        float(guidance), int(use_cfg), int(apg), float(apg_thr), int(use_graph)),
-              "flite_dit_sample")
+        self._check_sp(self.lib.flite_dit_sample(self.h, stream_ptr(acc.device), acc.data_ptr(), n_img, n, ta, da,
+                                                 float(guidance), int(use_cfg), int(apg), float(apg_thr),
+                                                 int(use_graph)), "flite_dit_sample")
         return acc
 
 

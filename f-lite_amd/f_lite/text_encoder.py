@@ -168,7 +168,10 @@ class T5Encoder(nn.Module):
         sd = {}
         for f in files:
             sd.update(load_file(str(f)))
-        m = cls.empty(device=device, dtype=torch_dtype, **cfg)
+        # config.json also holds transformers' own keys ("dtype"/"torch_dtype", "architectures", ...): keep only
+        # the architecture fields (the loader's torch_dtype / device win)
+        arch = {k: v for k, v in cfg.items() if k in T5_PRESETS["t5-xxl"] or k == "feed_forward_proj"}
+        m = cls.empty(device=device, dtype=torch_dtype, **arch)
         if "shared.weight" not in sd and "encoder.embed_tokens.weight" in sd:
             sd["shared.weight"] = sd["encoder.embed_tokens.weight"]
         sd.setdefault("encoder.embed_tokens.weight", sd["shared.weight"])

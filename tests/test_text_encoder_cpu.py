@@ -80,3 +80,20 @@ def test_synthetic_tokenizer():
     assert ids[0, 5] == 1 and (ids[0, 6:] == 0).all()
     long = tok(text=["x" * 2000], max_length=512, truncation=True, pad_to_multiple_of=8)
     assert long["input_ids"].shape == (1, 512) and long["input_ids"][0, -1] == 1
+
+
+def test_save_and_load_local_folder(tmp_path):
+    """T5Encoder.save_pretrained -> from_pretrained (config.json + model.safetensors, T5EncoderModel keys); a
+    transformers-saved folder loads the same way."""
+    from f_lite.text_encoder import T5Encoder
+
+    m = hf_tiny()
+    m.save_pretrained(str(tmp_path / "hf"), safe_serialization=True)
+    ours = T5Encoder.from_pretrained(str(tmp_path / "hf"), torch_dtype=torch.float32, device="cpu")
+    want = m.state_dict()
+    got = ours.state_dict()
+    assert set(got) == set(want)
+    assert all(torch.equal(got[k], want[k].float()) for k in want)
+    ours.save_pretrained(tmp_path / "ours")
+    again = T5Encoder.from_pretrained(tmp_path / "ours", torch_dtype=torch.float32, device="cpu")
+    assert all(torch.equal(again.state_dict()[k], got[k]) for k in got)
