@@ -230,10 +230,11 @@ def test_attention_spike_rescale():
     assert rel(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("D", [512, 3072])  # 3072: the one-workgroup-per-row kernel of the DiT width
+# 3072: the one-workgroup-per-row kernel of the DiT width; 602 rows: a partial last group of the 4-row kernel
+@pytest.mark.parametrize("D", [512, 3072])
 @pytest.mark.parametrize("in_bf16", [False, True])
 def test_rmsnorm_modulate(in_bf16, D):
-    rows, T = 600, 250
+    rows, T = 602, 250
     x = torch.randn(rows, D, device=DEV) * 3
     if in_bf16:
         x = x.bfloat16()
