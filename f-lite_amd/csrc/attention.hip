@@ -19,7 +19,7 @@
 // One workgroup per tile runs the 24 tails as a 4th round on 24 CUs (a 25 % loss). With the bounded softmax
 // (fixed shift, so partial sums add without rescaling) and a caller workspace, the tail of each (sequence,
 // head) is instead cut into n_split contiguous ranges of key tiles ("phase B" workgroups, queued after the
-// full tiles, one short round). Each writes its unnormalised O and row sums to its own slab (write-through
+// full tiles, one short round; before them when the key range is short, split_first). Each writes its unnormalised O and row sums to its own slab (write-through
 // stores) and bumps the pair's counter; the last arriver adds the slabs in slab order (deterministic: the
 // same sum on every launch), normalises and stores the rows, and resets the counter for the next launch.
 #include <algorithm>
@@ -46,7 +46,8 @@ constexpr int SLAB_FLOATS = SLAB_O_FLOATS + 4 * 64;
 constexpr long SLAB_BYTES = (long)SLAB_FLOATS * 4;
 constexpr long CNT_BYTES = 4096;  // counter block at the workspace start (1024 (sequence, head) pairs)
 constexpr int MAX_SPLIT = 16;     // key ranges per tail
-constexpr int MIN_SPLIT_KEYS = 16 * KT;  // shorter key ranges: the tail round is cheaper than the hand-off
+constexpr int MIN_SPLIT_KEYS = 4 * KT;     // shorter key ranges: the tail round is cheaper than the hand-off
+constexpr int SPLIT_FIRST_KEYS = 16 * KT;  // below this the tail chunks go first (see attn_fwd)
 
 __device__ __forceinline__ s16x4 ds_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(p));
@@ -132,15 +133,17 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // Work decode. Phase A (blocks [0, nA)): one 128-row q-tile of one (sequence, head), all keys. Phase B
-  // (the rest): key range `chunk` of the tail rows [n_main*QT, q_len) of one (sequence, head).
+  // Work decode. Phase A (blocks [0, nA), or the last nA with split_first): one 128-row q-tile of one (sequence,
+  // head), all keys. Phase B (the rest): key range `chunk` of the tail rows [n_main*QT, q_len) of one pair.
   // Each phase is remapped XCD-aware, so consecutive workgroups of one XCD share a (sequence, head) and its
   // K/V stream in L2.
   int b, h, q0, chunk = -1;
   {
     const int nA = p.B * p.H * p.n_main;
-    const bool phase_a = (int)blockIdx.x < nA;
-    const int v = phase_a ? xcd_remap(blockIdx.x, nA) : xcd_remap(blockIdx.x - nA, gridDim.x - nA);
+    const int nB = (int)gridDim.x - nA;
+    const int b0 = p.split_first ? 0 : nA;  // first block of phase B
+    const bool phase_a = p.split_first ? (int)blockIdx.x >= nB : (int)blockIdx.x < nA;
+    const int v = phase_a ? xcd_remap(blockIdx.x - (p.split_first ? nB : 0), nA) : xcd_remap(blockIdx.x - b0, nB);
     int pair;
     if (phase_a) {
       q0 = (v % p.n_main) * QT;
@@ -670,6 +673,11 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
     if (S >= 2) {
       q.n_main = p.max_q / QT;
       q.n_split = S;
+      // Short key ranges (cross-attention, 512 keys: 8 tiles) leave every tail chunk mostly prologue, so a
+      // 4th round of them costs almost a full round. Dispatched first instead, they finish early and the CUs
+      // that ran them take fewer full q-tiles: 89.7 -> 83.3 us at T = 4112, L = 512 (profiles/r02u). Long
+      // key ranges keep the chunks last (first cost self-attention 1.5 %).
+      q.split_first = p.max_k > 0 && p.max_k < SPLIT_FIRST_KEYS;
     }
   }
   dim3 grid(pairs * (q.n_main + q.n_split));

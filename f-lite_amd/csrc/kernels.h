@@ -76,6 +76,7 @@ struct AttnParams {
   void* split_ws = nullptr;
   long split_ws_bytes = 0;
   int n_main = 0, n_split = 0;  // set by the launcher
+  int split_first = 0;          // set by the launcher: tail chunks dispatched before the full q-tiles
 };
 
 int attn_fwd(const AttnParams& p, hipStream_t stream);

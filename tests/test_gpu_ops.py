@@ -185,7 +185,8 @@ def test_attention_varlen(lens_q, lens_k, bounded):
 
 # Tail split (attention.hip "Schedule"): the partial last q-tile of every (sequence, head) is cut by key ranges
 # over the chip and reduced in slab order. Cases: the DiT self (T = 4112: 16-row tails) and cross shapes, ragged
-# tails of up to 127 rows, more chunks than key tiles (empty chunks), no keys at all.
+# tails of up to 127 rows, more chunks than key tiles (empty chunks), no keys at all; with max_k, the engine's
+# policy (cross-attention: tail chunks first).
 @pytest.mark.parametrize("lens_q,lens_k,H", [([4112, 4112], None, 12), ([4112, 4112], [512, 512], 12),
                                              ([300, 200], None, 2), ([130, 255], [24, 17], 2),
                                              ([1000, 77], [700, 0], 3), ([50], [4096], 1)])
@@ -212,6 +213,12 @@ def test_attention_tail_split(lens_q, lens_k, H):
     # deterministic (fixed slab order) and the workspace is left zeroed for the next launch
     again = nat.attn_varlen(*args, max_score=16.5, workspace=ws)
     assert torch.equal(split, again)
+    assert int(ws[:4096].view(torch.int32).abs().sum().item()) == 0
+    # with the key length known (the engine's call): key ranges of 256-1023 keys dispatch their tail chunks
+    # before the full q-tiles (split_first), shorter ones do not split
+    policy = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
+    assert rel(policy, whole) < 5e-3
+    assert torch.equal(policy, nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k)))
     assert int(ws[:4096].view(torch.int32).abs().sum().item()) == 0
 
 
