@@ -65,7 +65,9 @@ def test_gemm_swiglu():
     assert rel(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("shared", [False, True])
+# segments of 300 rows: some waves' rows straddle a segment boundary (per-row gate path), the others take the
+# one-round-trip path (rows 0-3 of x through LDS); shared gate rows; no gate at all
+@pytest.mark.parametrize("shared", [False, True, None])
 def test_gemm_gated_residual(shared):
     M, N, K, T = 1000, 768, 256, 300
     a = torch.randn(M, K, device=DEV).bfloat16()
@@ -77,10 +79,10 @@ def test_gemm_gated_residual(shared):
     y = a.float() @ w.float().t() + b.float()
     ref = x0.clone()
     for s in range(nseg):
-        ref[s * T:(s + 1) * T] += y[s * T:(s + 1) * T] * gate[0 if shared else s]
+        ref[s * T:(s + 1) * T] += y[s * T:(s + 1) * T] * (1.0 if shared is None else gate[0 if shared else s])
     x = x0.clone()
-    nat.gemm(a, w, b, out=x, epilogue=nat.EPI_RESID_F32, gate=gate, gate_seg_stride=0 if shared else N,
-             rows_per_seg=T)
+    nat.gemm(a, w, b, out=x, epilogue=nat.EPI_RESID_F32, gate=None if shared is None else gate,
+             gate_seg_stride=0 if shared else N, rows_per_seg=T)
     assert rel(x, ref) < 1e-5
 
 
