@@ -382,6 +382,14 @@ int flite_gemm_fp8(void* stream, int M, int N, int K, const void* A8, long lda, 
                    long a_rows_pad, const void* W8, long ldw, const void* w_scales, long w_rows_pad,
                    const void* bias, int epilogue, void* out, long ldo, void* out_scales, long out_rows_pad,
                    const float* gate, long gate_seg_stride, int rows_per_seg) {
+  return flite_gemm_fp8_ws(stream, M, N, K, A8, lda, a_scales, a_rows_pad, W8, ldw, w_scales, w_rows_pad, bias,
+                           epilogue, out, ldo, out_scales, out_rows_pad, gate, gate_seg_stride, rows_per_seg, nullptr);
+}
+
+int flite_gemm_fp8_ws(void* stream, int M, int N, int K, const void* A8, long lda, const void* a_scales,
+                      long a_rows_pad, const void* W8, long ldw, const void* w_scales, long w_rows_pad,
+                      const void* bias, int epilogue, void* out, long ldo, void* out_scales, long out_rows_pad,
+                      const float* gate, long gate_seg_stride, int rows_per_seg, void* workspace) {
   FLITE_REQUIRE(A8 && a_scales && W8 && w_scales && out, "flite_gemm_fp8: null argument");
   GemmFp8Params p;
   p.A = (const uint8_t*)A8;
@@ -403,6 +411,11 @@ int flite_gemm_fp8(void* stream, int M, int N, int K, const void* A8, long lda, 
   p.M = M;
   p.N = N;
   p.K = K;
+  const int G = gemm_sk_workspace_cus();
+  if (workspace != nullptr && G > 0) {  // the bf16 workspace layout: partial tiles, then one flag per CU
+    p.sk_ws = (float*)workspace;
+    p.sk_flags = (int*)((char*)workspace + (size_t)G * 256 * 256 * sizeof(float));
+  }
   return gemm_fp8(p, epilogue, (hipStream_t)stream);
 }
 

@@ -723,6 +723,9 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
       g.rope_cols = rope_cols;
       g.rope = rope_axes();
     }
+    static const bool no_sk = getenv("FLITE_GEMM_NO_STREAM_K") != nullptr;  // A/B switch, as gemm()
+    g.sk_ws = no_sk ? nullptr : sk_ws_;
+    g.sk_flags = no_sk ? nullptr : sk_flags_;
     return gemm_fp8(g, epi, s);
   };
   auto attn = [&](const bf16_t* qp, long ldq, const bf16_t* kp, const bf16_t* vp, long ldkv, const int* cu_k,

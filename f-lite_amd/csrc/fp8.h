@@ -57,6 +57,12 @@ struct GemmFp8Params {
   RopeAxes rope;
   int rope_cols = 0, norm_cols = 0;
   float norm_eps = 1e-6f;
+  // stream-K workspace (optional, gemm.hip layout: fp32 partial tiles [CUs][256*256] + int flags [CUs], zeroed):
+  // the launcher may cut a partial last wave of 256x256 tiles into equal k-ranges (stream_k.h)
+  float* sk_ws = nullptr;
+  int* sk_flags = nullptr;
+  int sk_tiles = 0;  // set by the launcher
+  int sk_wgs = 0;    // set by the launcher
 };
 
 int gemm_fp8(const GemmFp8Params& p, int epi, hipStream_t s);

@@ -21,6 +21,7 @@
 
 #include "fp8.h"
 #include "kernels.h"
+#include "stream_k.h"
 
 namespace flite {
 
@@ -268,16 +269,20 @@ struct Fp8Cta {
     stage(wave_m == 1 ? kt + 2 : ke, BUF);
   }
 
-  __device__ __forceinline__ void mainloop(f32x4 (&acc)[8][4], int nk) {
+  // acc = the k-tiles [kb, kend) of the tile set up by setup_tile
+  __device__ __forceinline__ void mainloop(f32x4 (&acc)[8][4], int kb, int kend) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    ke = nk;
-    stage(0, 0);
-    stage(1, 1);
-    // this wave's copies of tile 0 are the oldest: leave tile 1's (8, +1 scale piece for waves 0, 1) in flight
-    if (nk <= 1)
+    ke = kend;
+    // the previous tile's last reads / DMA of this workgroup must be done before the buffers are refilled
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stage(kb, 0);
+    stage(kb + 1, 1);
+    // this wave's copies of tile kb are the oldest: leave kb+1's (8, +1 scale piece for waves 0, 1) in flight
+    if (kend - kb <= 1)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if (wave < 2)
       asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
@@ -295,12 +300,12 @@ struct Fp8Cta {
     a1 = rd_a<0>(1);
     s0 = rd_as<0>(0);
     s1 = rd_as<0>(1);
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
+    int kt = kb;
+    for (; kt + 1 < kend; kt += 2) {
       ktile<0>(acc, wf, ws, a0, s0, a1, s1, kt);
       ktile<1>(acc, wf, ws, a0, s0, a1, s1, kt + 1);
     }
-    if (kt < nk) ktile<0>(acc, wf, ws, a0, s0, a1, s1, kt);
+    if (kt < kend) ktile<0>(acc, wf, ws, a0, s0, a1, s1, kt);
   }
 
   // RoPE + QK-norm, as gemm.hip's qkv_norm_epilogue: RoPE tiles (n0 < rope_cols) hold the q/k heads in rope_perm
@@ -465,22 +470,6 @@ struct Fp8Cta {
   }
 };
 
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
-__device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0, int& n0, int bm) {
-  constexpr int GROUP = 6;
-  const int group_size = GROUP * num_n;
-  const int gid = L / group_size;
-  const int first_m = gid * GROUP;
-  const int gm = min(num_m - first_m, GROUP);
-  const int rem = L - gid * group_size;
-  m0 = (first_m + rem % gm) * bm;
-  n0 = (rem / gm) * BN;
-}
-
 template <int EPI, int MI>
 __global__ __launch_bounds__(NT, 2) void gemm_fp8_kernel(GemmFp8Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -488,17 +477,25 @@ __global__ __launch_bounds__(NT, 2) void gemm_fp8_kernel(GemmFp8Params p) {
   Cta c(p, smem);
   const int num_m = (p.M + Cta::WM * 2 - 1) / (Cta::WM * 2);
   const int num_n = (p.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  int m0, n0;
-  tile_origin(wg, num_m, num_n, m0, n0, Cta::WM * 2);
+  const int nk = p.K / 128;
+  const int wg = sk::xcd_remap(blockIdx.x, gridDim.x);
   f32x4 acc[8][4];
+  if constexpr (MI == 8) {
+    if (p.sk_tiles > 0) {  // persistent grid, one workgroup per CU (launch8)
+      sk::stream_k_body<NT>(c, acc, num_m, num_n, nk, wg);
+      return;
+    }
+  }
+  int m0, n0;
+  sk::tile_origin(wg, num_m, num_n, m0, n0, Cta::WM * 2, BN);
   c.setup_tile(m0, n0);
-  c.mainloop(acc, p.K / 128);
+  c.mainloop(acc, 0, nk);
   c.epilogue(acc, m0, n0);
 }
 
 int g_cus = 0;
 bool g_attrs = false;
+bool g_sk_ok = false;  // every workgroup of a one-per-CU grid is resident at once (stream-K waits on peers)
 
 template <int EPI>
 hipError_t set_attrs8() {
@@ -518,6 +515,10 @@ int init8() {
   int dev = 0;
   FLITE_HIP_CHECK(hipGetDevice(&dev));
   FLITE_HIP_CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev));
+  int per_cu = 0;
+  FLITE_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_fp8_kernel<EPI8_RESID_F32, 8>, NT,
+                                                              LDS_BYTES));
+  g_sk_ok = per_cu >= 1;
   g_attrs = true;
   return 0;
 }
@@ -532,9 +533,15 @@ bool bm224(const GemmFp8Params& p) {
 }
 
 template <int EPI>
-void launch8(const GemmFp8Params& p, hipStream_t s) {
+void launch8(GemmFp8Params p, hipStream_t s) {
   const int num_n = (p.N + BN - 1) / BN;
-  if (bm224(p)) {
+  const int T = (p.M + 255) / 256 * num_n;
+  p.sk_tiles = (p.sk_ws != nullptr && p.sk_flags != nullptr && g_sk_ok)
+                   ? sk::choose_sk_tiles(T, p.K / 128, g_cus, &p.sk_wgs)
+                   : 0;
+  if (p.sk_tiles) {
+    hipLaunchKernelGGL((gemm_fp8_kernel<EPI, 8>), dim3(g_cus), dim3(NT), LDS_BYTES, s, p);
+  } else if (bm224(p)) {
     hipLaunchKernelGGL((gemm_fp8_kernel<EPI, 7>), dim3((p.M + 223) / 224 * num_n), dim3(NT), LDS_BYTES, s, p);
   } else {
     hipLaunchKernelGGL((gemm_fp8_kernel<EPI, 8>), dim3((p.M + 255) / 256 * num_n), dim3(NT), LDS_BYTES, s, p);

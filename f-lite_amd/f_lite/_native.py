@@ -92,6 +92,8 @@ SIGNATURES = {
     "flite_quant_fp8_gateup": (_i, [_vp, _vp, _vp, _l, _i, _i, _vp, _vp]),
     "flite_gemm_fp8": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _l, _vp, _l, _vp, _i, _vp, _l, _vp, _l, _vp, _l,
                             _i]),
+    "flite_gemm_fp8_ws": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _l, _vp, _l, _vp, _i, _vp, _l, _vp, _l, _vp,
+                               _l, _i, _vp]),
     "flite_rmsnorm_modulate_fp8": (_i, [_vp, _vp, _l, _vp, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_dit_enable_fp8": (_i, [_vp, _vp, _i]),
     "flite_dit_set_sequence_parallel": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -341,9 +343,10 @@ def quant_fp8_gateup(gate: torch.Tensor, up: torch.Tensor):
 
 
 def gemm_fp8(a8, a_sc, w8, w_sc, bias=None, *, out=None, epilogue=EPI8_STORE_BF16, out_sc=None, gate=None,
-             gate_seg_stride=0, rows_per_seg=1):
+             gate_seg_stride=0, rows_per_seg=1, workspace=None):
     """C = dequant(a8) . dequant(w8)^T on the MXFP8 MFMA. a8 [M, K] / w8 [N, K] uint8 with scales from
-    quant_fp8_rows (w8/w_sc of the SwiGLU epilogue from quant_fp8_gateup, N = 2F)."""
+    quant_fp8_rows (w8/w_sc of the SwiGLU epilogue from quant_fp8_gateup, N = 2F). `workspace` (gemm_workspace)
+    enables the stream-K split of a partial last wave of tiles."""
     lib = load()
     M, K = a8.shape
     N = w8.shape[0]
@@ -356,11 +359,14 @@ def gemm_fp8(a8, a_sc, w8, w_sc, bias=None, *, out=None, epilogue=EPI8_STORE_BF1
         out = torch.empty(M, N, device=a8.device, dtype=torch.bfloat16 if epilogue == EPI8_STORE_BF16 else torch.float32)
     for t, n in ((a8, "a8"), (a_sc, "a_scales"), (w8, "w8"), (w_sc, "w_scales"), (out, "out")):
         require_gpu(t, n, contiguous=False)
-    check(lib.flite_gemm_fp8(stream_ptr(a8.device), M, N, K, a8.data_ptr(), a8.stride(0), a_sc.data_ptr(),
-                             a_sc.shape[1], w8.data_ptr(), w8.stride(0), w_sc.data_ptr(), w_sc.shape[1], _ptr(bias),
-                             epilogue, out.data_ptr(), out.stride(0), _ptr(out_sc),
-                             out_sc.shape[1] if out_sc is not None else 0, _ptr(gate), gate_seg_stride, rows_per_seg),
-          "flite_gemm_fp8")
+    if workspace is not None:
+        require_gpu(workspace, "workspace", contiguous=True)
+    check(lib.flite_gemm_fp8_ws(stream_ptr(a8.device), M, N, K, a8.data_ptr(), a8.stride(0), a_sc.data_ptr(),
+                                a_sc.shape[1], w8.data_ptr(), w8.stride(0), w_sc.data_ptr(), w_sc.shape[1],
+                                _ptr(bias), epilogue, out.data_ptr(), out.stride(0), _ptr(out_sc),
+                                out_sc.shape[1] if out_sc is not None else 0, _ptr(gate), gate_seg_stride,
+                                rows_per_seg, _ptr(workspace)),
+          "flite_gemm_fp8_ws")
     return (out, out_sc) if epilogue == EPI8_SWIGLU_FP8 else out
 
 

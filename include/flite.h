@@ -135,6 +135,13 @@ int flite_gemm_fp8(void* stream, int M, int N, int K, const void* A8, long lda, 
                    long a_rows_pad, const void* W8, long ldw, const void* w_scales, long w_rows_pad,
                    const void* bias, int epilogue, void* out, long ldo, void* out_scales, long out_rows_pad,
                    const float* gate, long gate_seg_stride, int rows_per_seg);
+/* flite_gemm_fp8 with the stream-K workspace of flite_gemm_bf16_ws (flite_gemm_workspace_bytes, zero-filled
+ * once, left zeroed; launches sharing it must be stream-ordered): the launcher may cut a partial last wave of
+ * 256x256 tiles into equal k-ranges over the CUs. */
+int flite_gemm_fp8_ws(void* stream, int M, int N, int K, const void* A8, long lda, const void* a_scales,
+                      long a_rows_pad, const void* W8, long ldw, const void* w_scales, long w_rows_pad,
+                      const void* bias, int epilogue, void* out, long ldo, void* out_scales, long out_rows_pad,
+                      const float* gate, long gate_seg_stride, int rows_per_seg, void* workspace);
 /* flite_rmsnorm_modulate with MXFP8 output (fp32 x): y8 [rows, dim] bytes (row stride ldy) + scales. */
 int flite_rmsnorm_modulate_fp8(void* stream, const float* x, long ldx, void* y8, long ldy, void* y_scales,
                                long rows_pad, const void* w, const float* shift, const float* scale,

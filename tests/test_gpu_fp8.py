@@ -104,6 +104,41 @@ def test_gemm_fp8(M, N, K, epi):
         assert err < 4e-3, err  # bf16 output rounding
 
 
+# Stream-K (flite_gemm_fp8_ws, stream_k.h): a partial last wave of 256x256 tiles cut into k-ranges over the CUs
+# (the 10B down projection at 1024^2, and a 12-tile grid split ~4 ways per tile). Every epilogue runs in the
+# finisher: fp32 residual, bf16 store, SwiGLU -> e4m3.
+@pytest.mark.parametrize("M,N,K", [(8224, 3072, 12288), (1000, 768, 16384)])
+def test_gemm_fp8_stream_k(M, N, K):
+    g = torch.Generator().manual_seed(K + M)
+    a8, asc = nat.quant_fp8_rows(torch.randn(M, K, generator=g).bfloat16().to(DEV))
+    w8, wsc = nat.quant_fp8_rows((torch.randn(N, K, generator=g) * 0.02).bfloat16().to(DEV))
+    bias = (torch.randn(N, generator=g) * 0.1).bfloat16().to(DEV)
+    ws = nat.gemm_workspace(DEV)
+    ref = dequant(a8, asc).double() @ dequant(w8, wsc).double().t() + bias.cpu().double()
+    gate = torch.ones(1, N, device=DEV)
+    outs = []
+    for w_ in (None, ws, ws):
+        x = torch.zeros(M, N, device=DEV)
+        nat.gemm_fp8(a8, asc, w8, wsc, bias, out=x, epilogue=nat.EPI8_RESID_F32, gate=gate, gate_seg_stride=0,
+                     rows_per_seg=M, workspace=w_)
+        outs.append(x.cpu())
+    dp, sk, sk2 = outs
+    for o in (dp, sk):
+        assert ((o.double() - ref).norm() / ref.norm()).item() < 1e-4
+    assert not torch.equal(sk, dp)  # the split ran (another fp32 summation order)
+    assert torch.equal(sk, sk2)  # deterministic
+    n_cu = ws.numel() // (256 * 256 * 4 + 4)
+    assert int(ws[n_cu * 256 * 256 * 4:].view(torch.int32).abs().sum().item()) == 0  # flags back to 0
+    st = nat.gemm_fp8(a8, asc, w8, wsc, bias, workspace=ws)
+    assert ((st.cpu().double() - ref).norm() / ref.norm()).item() < 4e-3
+    F = N // 2
+    gu8, gusc = nat.quant_fp8_gateup((torch.randn(F, K, generator=g) * 0.02).bfloat16().to(DEV),
+                                     (torch.randn(F, K, generator=g) * 0.02).bfloat16().to(DEV))
+    h_dp, s_dp = nat.gemm_fp8(a8, asc, gu8, gusc, epilogue=nat.EPI8_SWIGLU_FP8)
+    h_sk, s_sk = nat.gemm_fp8(a8, asc, gu8, gusc, epilogue=nat.EPI8_SWIGLU_FP8, workspace=ws)
+    assert psnr(dequant(h_sk, s_sk), dequant(h_dp, s_dp)) > 40
+
+
 def test_gemm_fp8_swiglu():
     M, F, K = 1000, 1024, 512
     g = torch.Generator().manual_seed(9)
