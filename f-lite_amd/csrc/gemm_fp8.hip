@@ -539,6 +539,12 @@ void launch8(GemmFp8Params p, hipStream_t s) {
   p.sk_tiles = (p.sk_ws != nullptr && p.sk_flags != nullptr && g_sk_ok)
                    ? sk::choose_sk_tiles(T, p.K / 128, g_cus, &p.sk_wgs)
                    : 0;
+  static const bool sk_always = getenv("FLITE_FP8_SK_ALWAYS") != nullptr;  // A/B switch for measurements
+  if (sk_always && p.sk_ws != nullptr && p.sk_flags != nullptr && g_sk_ok && T % g_cus != 0 &&
+      (long)(T % g_cus) * (p.K / 128) >= 2L * g_cus) {
+    p.sk_tiles = T % g_cus;
+    p.sk_wgs = g_cus;
+  }
   if (p.sk_tiles) {
     hipLaunchKernelGGL((gemm_fp8_kernel<EPI, 8>), dim3(g_cus), dim3(NT), LDS_BYTES, s, p);
   } else if (bm224(p)) {
