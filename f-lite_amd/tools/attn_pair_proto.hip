@@ -125,7 +125,7 @@ __global__ __launch_bounds__(NT, 1) void attn_pair_kernel(P p) {
   const long k_base = (long)k_start * p.k_row_stride + (long)h * p.k_head_stride;
   const long v_base = (long)k_start * p.v_row_stride + (long)h * p.v_head_stride;
   const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr_of(smem));
-  unsigned k_src[4], v_src[4];
+  unsigned k_src[4], v_src[4];  // (dead in the ping-pong build: only the one-phase loop's copies use them)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = 2 * (wave * 4 + i) + hh;
@@ -299,6 +299,134 @@ __global__ __launch_bounds__(NT, 1) void attn_pair_kernel(P p) {
     }
     ATTN_TILE_SYNC();
   };
+#ifndef PAIR_PINGPONG
+#define PAIR_PINGPONG 0
+#endif
+#if PAIR_PINGPONG
+  // Ping-pong: waves 0-3 (X, key half 0) and 4-7 (Y, key half 1) run half an iteration apart, so the two waves
+  // of a SIMD are always in different phases -- one in phase A (K reads, S MFMAs, LDS-DMA), the other in phase B
+  // (V reads, O MFMAs, softmax). Slot t: X runs A_{t/2} (t even) / B_{(t-1)/2} (t odd); Y runs B_{t/2-1} /
+  // A_{(t-1)/2}. X stages every K tile, Y every V tile (8 pieces per wave, in their A slots); a role waits for
+  // its copies at the barrier that ends its B slot, two slots before their first reader.
+  const bool X = hf == 0;
+  unsigned src8[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = 2 * ((wave & 3) * 8 + i) + hh;
+    const int pos = lane & 31;
+    src8[i] = X ? (unsigned)(row * p.k_row_stride * 2 + ((pos ^ (row & 15)) * 16))
+                : (unsigned)(row * p.v_row_stride * 2 + (((((pos >> 2) ^ (row & 3)) << 2) | (pos & 3)) * 16));
+  }
+  // phase A for this wave: S of tile tk1 (K buffer KB) and, DMA, the 8 pieces of this role's tile td into
+  // buffer DB (X: K, Y: V)
+  auto phase_a_pp = [&](auto kb_, auto db_, auto dma_, int td, bool live) {
+    constexpr int KB = decltype(kb_)::value, DB = decltype(db_)::value;
+    constexpr bool DMA = decltype(dma_)::value;
+    const char* Kb = kbase + KB * TILE;
+    i32x4 rs = {0, 0, 0, 0};
+    if constexpr (DMA) rs = X ? rsrc_tile(p.k, k_base, p.k_row_stride, td, live) : rsrc_tile(p.v, v_base, p.v_row_stride, td, live);
+    const unsigned dst = lds0 + DB * TILE + (wave & 3) * 8 * 1024 + (X ? K_OFF : V_OFF);
+    bf16x8 kf[16];
+#pragma unroll
+    for (int s = 0; s < KAHEAD; ++s) kf[s] = *(const bf16x8*)(Kb + koff(s));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s + KAHEAD < 16) kf[s + KAHEAD] = *(const bf16x8*)(Kb + koff(s + KAHEAD));
+      __builtin_amdgcn_sched_barrier(0);
+      if (s == 0)
+        mfma_s_first(sh, kf[0], qf[0]);
+      else
+        mfma_s(sh, kf[s], qf[s]);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DMA) {
+        if ((s & 1) == 0) blds16(rs, src8[s >> 1], dst + (s >> 1) * 1024);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    mfma_read_fence(sh);
+  };
+  auto slot_sync = [&](bool wait) {
+    if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  // A_j for this wave: S_{j+1} from Kbuf[(j+1)&1]; X copies K_{j+2} into Kbuf[j&1], Y V_{j+1} into Vbuf[(j+1)&1]
+  auto A = [&](auto pj_, int j) {
+    constexpr int PJ = decltype(pj_)::value;
+    if (X)
+      phase_a_pp(std::integral_constant<int, PJ ^ 1>{}, std::integral_constant<int, PJ>{}, BT{}, j + 2, j + 2 < nt);
+    else
+      phase_a_pp(std::integral_constant<int, PJ ^ 1>{}, std::integral_constant<int, PJ ^ 1>{}, BT{}, j + 1, j + 1 < nt);
+  };
+  // B_j: O += V_j P_j (own P in pc, the partner's from slot parity j&1), softmax of S_{j+1} (EX) into pn, published
+  // to parity (j+1)&1
+  auto B = [&](auto pj_, auto ex_, u32x4 (&pc)[2], u32x4 (&pn)[2]) {
+    constexpr int PJ = decltype(pj_)::value;
+    constexpr bool EX = decltype(ex_)::value;
+    phase_b(std::integral_constant<int, PJ>{}, std::integral_constant<int, PJ>{}, ex_, pc, pn);
+    if constexpr (EX) publish(pn, PJ ^ 1);
+  };
+  if (nt > 0) {
+    {  // X: K_0 into Kbuf 0 and K_1 into Kbuf 1; Y: V_0 into Vbuf 0 (8 pieces per tile and wave, as in the loop)
+      const unsigned dst = lds0 + (wave & 3) * 8 * 1024;
+      if (X) {
+        const i32x4 k0 = rsrc_tile(p.k, k_base, p.k_row_stride, 0, true);
+        const i32x4 k1 = rsrc_tile(p.k, k_base, p.k_row_stride, 1, nt > 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          blds16(k0, src8[i], dst + i * 1024 + K_OFF);
+          blds16(k1, src8[i], dst + TILE + i * 1024 + K_OFF);
+        }
+      } else {
+        const i32x4 v0 = rsrc_tile(p.v, v_base, p.v_row_stride, 0, true);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) blds16(v0, src8[i], dst + i * 1024 + V_OFF);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    phase_a(I0{}, I0{}, I0{}, BF{}, 0, false, 0, false);  // S_0
+    {
+      float e_prev = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) softmax_elem(pa, e, e_prev);
+    }
+    publish(pa, 0);
+    __syncthreads();
+    // pa holds P_j for even j, pb for odd j
+    int j = 0;
+    for (; j + 2 < nt; j += 2) {
+      // iteration j (even)
+      if (X) A(I0{}, j); else if (j > 0) B(I1{}, BT{}, pb, pa);   // Y: B_{j-1}
+      slot_sync(!X);
+      if (X) B(I0{}, BT{}, pa, pb); else A(I0{}, j);
+      slot_sync(X);
+      // iteration j + 1 (odd)
+      if (X) A(I1{}, j + 1); else B(I0{}, BT{}, pa, pb);           // Y: B_j
+      slot_sync(!X);
+      if (X) B(I1{}, BT{}, pb, pa); else A(I1{}, j + 1);
+      slot_sync(X);
+    }
+    // the last one or two tiles (no S beyond tile nt - 1)
+    if (nt - j == 2) {
+      if (X) A(I0{}, j); else if (j > 0) B(I1{}, BT{}, pb, pa);
+      slot_sync(!X);
+      if (X) B(I0{}, BT{}, pa, pb); else A(I0{}, j);
+      slot_sync(X);
+      if (X) { /* no A_{nt-1} */ } else B(I0{}, BT{}, pa, pb);
+      slot_sync(!X);
+      if (X) B(I1{}, BF{}, pb, pa);
+      slot_sync(X);
+      if (!X) B(I1{}, BF{}, pb, pa);
+    } else {
+      if (!X && j > 0) B(I1{}, BT{}, pb, pa);
+      slot_sync(!X);
+      if (X) B(I0{}, BF{}, pa, pb);
+      slot_sync(X);
+      if (!X) B(I0{}, BF{}, pa, pb);
+    }
+  }
+#else
   if (nt > 0) {
     {  // K_0, V_0 into buffer 0, K_1 into Kbuf 1
       const i32x4 k0 = rsrc_tile(p.k, k_base, p.k_row_stride, 0, true);
@@ -333,6 +461,7 @@ __global__ __launch_bounds__(NT, 1) void attn_pair_kernel(P p) {
       iter(I0{}, BF{}, j);
     }
   }
+#endif
   o_acc_fence(o_acc);
   // row sums: lanes l, l + 32 hold complementary keys of the half; padded keys (zero rows of the last tile)
   // each added exp2(-m); then the partner's half through LDS
