@@ -303,11 +303,13 @@ __global__ __launch_bounds__(NT, 1) void attn_pair_kernel(P p) {
 #define PAIR_PINGPONG 0
 #endif
 #if PAIR_PINGPONG
-  // Ping-pong: waves 0-3 (X, key half 0) and 4-7 (Y, key half 1) run half an iteration apart, so the two waves
-  // of a SIMD are always in different phases -- one in phase A (K reads, S MFMAs, LDS-DMA), the other in phase B
-  // (V reads, O MFMAs, softmax). Slot t: X runs A_{t/2} (t even) / B_{(t-1)/2} (t odd); Y runs B_{t/2-1} /
-  // A_{(t-1)/2}. X stages every K tile, Y every V tile (8 pieces per wave, in their A slots); a role waits for
-  // its copies at the barrier that ends its B slot, two slots before their first reader.
+  // Ping-pong with ONE instruction stream: every wave runs  [A_j; barrier; B_j; wait own copies; barrier]  for
+  // j = 0.., but the key-half-1 waves (Y) pass one extra barrier first and the half-0 waves (X) one at the end,
+  // so between any two barriers X runs B_j while Y runs A_j, or X A_{j+1} while Y B_j: a SIMD's two waves are
+  // always in opposite phases (one reading K, doing S MFMAs and LDS-DMA; the other reading V, doing O MFMAs and
+  // the softmax). X stages the K tiles (K_{j+2} in A_j), Y the V tiles (V_{j+1} in A_j); each role waits for its
+  // own copies after its B phase, one phase before their first reader. The role is data only (source, stride,
+  // LDS region, tile offset): both roles share the code, so nothing is duplicated and nothing spills.
   const bool X = hf == 0;
   unsigned src8[8];
 #pragma unroll
@@ -317,15 +319,18 @@ __global__ __launch_bounds__(NT, 1) void attn_pair_kernel(P p) {
     src8[i] = X ? (unsigned)(row * p.k_row_stride * 2 + ((pos ^ (row & 15)) * 16))
                 : (unsigned)(row * p.v_row_stride * 2 + (((((pos >> 2) ^ (row & 3)) << 2) | (pos & 3)) * 16));
   }
-  // phase A for this wave: S of tile tk1 (K buffer KB) and, DMA, the 8 pieces of this role's tile td into
-  // buffer DB (X: K, Y: V)
-  auto phase_a_pp = [&](auto kb_, auto db_, auto dma_, int td, bool live) {
-    constexpr int KB = decltype(kb_)::value, DB = decltype(db_)::value;
-    constexpr bool DMA = decltype(dma_)::value;
+  const bf16_t* dsrc = X ? p.k + k_base : p.v + v_base;
+  const long dstride = X ? p.k_row_stride : p.v_row_stride;
+  const int dshift = X ? 2 : 1;
+  const unsigned dreg = lds0 + (X ? K_OFF : V_OFF) + (wave & 3) * 8 * 1024;
+  // A_j: S_{j+1} from Kbuf[KB]; this role's tile j + dshift into its buffer (tile & 1)
+  auto phase_a_pp = [&](auto kb_, int j) {
+    constexpr int KB = decltype(kb_)::value;
     const char* Kb = kbase + KB * TILE;
-    i32x4 rs = {0, 0, 0, 0};
-    if constexpr (DMA) rs = X ? rsrc_tile(p.k, k_base, p.k_row_stride, td, live) : rsrc_tile(p.v, v_base, p.v_row_stride, td, live);
-    const unsigned dst = lds0 + DB * TILE + (wave & 3) * 8 * 1024 + (X ? K_OFF : V_OFF);
+    const int td = j + dshift;
+    const long rows_left = td < nt ? k_len - (long)td * KT : 0;
+    const i32x4 rs = make_rsrc(dsrc + (long)td * KT * dstride, (unsigned)max(0L, min(rows_left * dstride * 2, 0x7fffffffL)));
+    const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)(dreg + (td & 1) * TILE));
     bf16x8 kf[16];
 #pragma unroll
     for (int s = 0; s < KAHEAD; ++s) kf[s] = *(const bf16x8*)(Kb + koff(s));
@@ -339,48 +344,31 @@ __global__ __launch_bounds__(NT, 1) void attn_pair_kernel(P p) {
       else
         mfma_s(sh, kf[s], qf[s]);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DMA) {
-        if ((s & 1) == 0) blds16(rs, src8[s >> 1], dst + (s >> 1) * 1024);
-      }
+      if ((s & 1) == 0) blds16(rs, src8[s >> 1], dst + (s >> 1) * 1024);
       __builtin_amdgcn_sched_barrier(0);
     }
     mfma_read_fence(sh);
   };
-  auto slot_sync = [&](bool wait) {
-    if (wait) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-  // A_j for this wave: S_{j+1} from Kbuf[(j+1)&1]; X copies K_{j+2} into Kbuf[j&1], Y V_{j+1} into Vbuf[(j+1)&1]
-  auto A = [&](auto pj_, int j) {
-    constexpr int PJ = decltype(pj_)::value;
-    if (X)
-      phase_a_pp(std::integral_constant<int, PJ ^ 1>{}, std::integral_constant<int, PJ>{}, BT{}, j + 2, j + 2 < nt);
-    else
-      phase_a_pp(std::integral_constant<int, PJ ^ 1>{}, std::integral_constant<int, PJ ^ 1>{}, BT{}, j + 1, j + 1 < nt);
-  };
-  // B_j: O += V_j P_j (own P in pc, the partner's from slot parity j&1), softmax of S_{j+1} (EX) into pn, published
-  // to parity (j+1)&1
+  // B_j: O += V_j P_j (own in pc, partner's from parity j & 1), softmax of S_{j+1} (EX) into pn -> parity (j+1) & 1
   auto B = [&](auto pj_, auto ex_, u32x4 (&pc)[2], u32x4 (&pn)[2]) {
     constexpr int PJ = decltype(pj_)::value;
     constexpr bool EX = decltype(ex_)::value;
     phase_b(std::integral_constant<int, PJ>{}, std::integral_constant<int, PJ>{}, ex_, pc, pn);
     if constexpr (EX) publish(pn, PJ ^ 1);
   };
+  auto end_b = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
   if (nt > 0) {
-    {  // X: K_0 into Kbuf 0 and K_1 into Kbuf 1; Y: V_0 into Vbuf 0 (8 pieces per tile and wave, as in the loop)
-      const unsigned dst = lds0 + (wave & 3) * 8 * 1024;
-      if (X) {
-        const i32x4 k0 = rsrc_tile(p.k, k_base, p.k_row_stride, 0, true);
-        const i32x4 k1 = rsrc_tile(p.k, k_base, p.k_row_stride, 1, nt > 1);
+    {  // X: K_0 into Kbuf 0 and K_1 into Kbuf 1; Y: V_0 into Vbuf 0
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          blds16(k0, src8[i], dst + i * 1024 + K_OFF);
-          blds16(k1, src8[i], dst + TILE + i * 1024 + K_OFF);
-        }
-      } else {
-        const i32x4 v0 = rsrc_tile(p.v, v_base, p.v_row_stride, 0, true);
+      for (int t = 0; t < 2; ++t) {
+        if (!X && t == 1) break;
+        const long rows_left = t < nt ? k_len - (long)t * KT : 0;
+        const i32x4 rs = make_rsrc(dsrc + (long)t * KT * dstride, (unsigned)max(0L, min(rows_left * dstride * 2, 0x7fffffffL)));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) blds16(v0, src8[i], dst + i * 1024 + V_OFF);
+        for (int i = 0; i < 8; ++i) blds16(rs, src8[i], dreg + t * TILE + i * 1024);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -393,38 +381,33 @@ __global__ __launch_bounds__(NT, 1) void attn_pair_kernel(P p) {
     }
     publish(pa, 0);
     __syncthreads();
+    if (!X) __syncthreads();  // Y runs one phase behind X
     // pa holds P_j for even j, pb for odd j
     int j = 0;
     for (; j + 2 < nt; j += 2) {
-      // iteration j (even)
-      if (X) A(I0{}, j); else if (j > 0) B(I1{}, BT{}, pb, pa);   // Y: B_{j-1}
-      slot_sync(!X);
-      if (X) B(I0{}, BT{}, pa, pb); else A(I0{}, j);
-      slot_sync(X);
-      // iteration j + 1 (odd)
-      if (X) A(I1{}, j + 1); else B(I0{}, BT{}, pa, pb);           // Y: B_j
-      slot_sync(!X);
-      if (X) B(I1{}, BT{}, pb, pa); else A(I1{}, j + 1);
-      slot_sync(X);
+      phase_a_pp(I1{}, j);
+      __syncthreads();
+      B(I0{}, BT{}, pa, pb);
+      end_b();
+      phase_a_pp(I0{}, j + 1);
+      __syncthreads();
+      B(I1{}, BT{}, pb, pa);
+      end_b();
     }
-    // the last one or two tiles (no S beyond tile nt - 1)
     if (nt - j == 2) {
-      if (X) A(I0{}, j); else if (j > 0) B(I1{}, BT{}, pb, pa);
-      slot_sync(!X);
-      if (X) B(I0{}, BT{}, pa, pb); else A(I0{}, j);
-      slot_sync(X);
-      if (X) { /* no A_{nt-1} */ } else B(I0{}, BT{}, pa, pb);
-      slot_sync(!X);
-      if (X) B(I1{}, BF{}, pb, pa);
-      slot_sync(X);
-      if (!X) B(I1{}, BF{}, pb, pa);
+      phase_a_pp(I1{}, j);
+      __syncthreads();
+      B(I0{}, BT{}, pa, pb);
+      end_b();
+      __syncthreads();  // (no A_{nt-1})
+      B(I1{}, BF{}, pb, pa);
+      end_b();
     } else {
-      if (!X && j > 0) B(I1{}, BT{}, pb, pa);
-      slot_sync(!X);
-      if (X) B(I0{}, BF{}, pa, pb);
-      slot_sync(X);
-      if (!X) B(I0{}, BF{}, pa, pb);
+      __syncthreads();  // (no A_{nt-1})
+      B(I0{}, BF{}, pa, pb);
+      end_b();
     }
+    if (X) __syncthreads();
   }
 #else
   if (nt > 0) {
