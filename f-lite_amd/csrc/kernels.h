@@ -166,4 +166,7 @@ int tile_to_uint8(const float* t, int tw, unsigned char* img, int img_w, int y0,
                   hipStream_t s);
 int to_uint8(const float* o, int ld, unsigned char* img, long hw, hipStream_t s);
 int pack_conv_weight(const bf16_t* w, bf16_t* o, int Cout, int Cin, int Cpad, hipStream_t s);
+// MXFP8 rows (e4m3 + one E8M0 scale per 32 K, scales row-major [rows][K/32]) <-> bf16 (the fp8 VAE weights)
+int mx_quant_rows_rm(const bf16_t* x, long rows, int K, uint8_t* q, uint8_t* sc, hipStream_t s);
+int mx_dequant_rows_rm(const uint8_t* q, const uint8_t* sc, long rows, int K, bf16_t* x, hipStream_t s);
 }  // namespace flite

@@ -6,6 +6,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "fp8.h"
 #include "kernels.h"
 
 namespace flite {
@@ -344,6 +345,82 @@ int tile_to_uint8(const float* t, int tw, unsigned char* img, int img_w, int y0,
 
 int to_uint8(const float* o, int ld, unsigned char* img, long hw, hipStream_t s) {
   hipLaunchKernelGGL(to_uint8_kernel, dim3(grid_of(hw * 3)), dim3(256), 0, s, o, ld, img, hw);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// fp8 weight storage (VaeEngine::enable_fp8_weights, the analogue of diffusers' layerwise casting with an fp8
+// storage dtype): a packed conv weight [Cout][K] -> OCP e4m3 bytes + one E8M0 scale per 32 consecutive K
+// (MXFP8, fp8.h rounding: bit-exact to oracle/flite_ref.py mx_quant), row-major scales [Cout][K/32]; and back
+// to bf16 right before the conv (exact: an e4m3 value times 2^e has at most 4 significant bits).
+__global__ __launch_bounds__(256) void mx_quant_rm_kernel(const bf16_t* x, long nblk, uint8_t* q, uint8_t* sc) {
+  const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  float v[32];
+  const u32x4* src = (const u32x4*)(x + b * 32);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const u32x4 w = src[c];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[8 * c + 2 * k] = __uint_as_float(w[k] << 16);
+      v[8 * c + 2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(v[j]));
+  const int e = mx_exp(amax);
+  const float inv = mx_inv(e);
+  u32x4 o[2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j >> 2][j & 3] = pack4_fp8(v + 4 * j, inv);
+  ((u32x4*)(q + b * 32))[0] = o[0];
+  ((u32x4*)(q + b * 32))[1] = o[1];
+  sc[b] = (uint8_t)(e + 127);
+}
+
+__global__ __launch_bounds__(256) void mx_dequant_rm_kernel(const uint8_t* q, const uint8_t* sc, long nblk,
+                                                            bf16_t* x) {
+  const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  const float scale = __uint_as_float((unsigned)sc[b] << 23);  // 2^(byte - 127); byte >= 0: e >= -127
+  const u32x4* src = (const u32x4*)(q + b * 32);
+  u32x4* dst = (u32x4*)(x + b * 32);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const u32x4 w = src[c];
+    u32x4 lo, hi;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[k], false);
+      const f32x2 d = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[k], true);
+      const unsigned p0 = pack2bf(a[0] * scale, a[1] * scale), p1 = pack2bf(d[0] * scale, d[1] * scale);
+      if (k < 2) {
+        lo[2 * k] = p0;
+        lo[2 * k + 1] = p1;
+      } else {
+        hi[2 * (k - 2)] = p0;
+        hi[2 * (k - 2) + 1] = p1;
+      }
+    }
+    dst[2 * c] = lo;
+    dst[2 * c + 1] = hi;
+  }
+}
+
+int mx_quant_rows_rm(const bf16_t* x, long rows, int K, uint8_t* q, uint8_t* sc, hipStream_t s) {
+  FLITE_REQUIRE(K % 32 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)q & 15) == 0, "mx_quant_rows: K % 32, 16-B");
+  const long nblk = rows * (K / 32);
+  hipLaunchKernelGGL(mx_quant_rm_kernel, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, x, nblk, q, sc);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int mx_dequant_rows_rm(const uint8_t* q, const uint8_t* sc, long rows, int K, bf16_t* x, hipStream_t s) {
+  FLITE_REQUIRE(K % 32 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)q & 15) == 0, "mx_dequant_rows: K % 32");
+  const long nblk = rows * (K / 32);
+  hipLaunchKernelGGL(mx_dequant_rm_kernel, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, s, q, sc, nblk, x);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

@@ -21,6 +21,18 @@ class VaeEngine {
     free_tiles();
   }
 
+  // fp8 weight storage (diffusers' layerwise casting with an fp8 storage dtype, compute bf16): every packed 3x3
+  // conv weight is kept as MXFP8 (e4m3 + one E8M0 scale per 32 of K) and expanded to bf16 right before its conv.
+  // 1.03 instead of 2 bytes per weight; the convs themselves run in bf16 as before.
+  int enable_fp8_weights(bool on) {
+    if (on != fp8_w_) {
+      fp8_w_ = on;
+      packed_.clear();  // re-pack (and re-allocate) on the next prepare
+    }
+    return 0;
+  }
+  bool fp8_weights() const { return fp8_w_; }
+
   int bind(const std::string& name, const void* p, long n) {
     FLITE_REQUIRE(p != nullptr && ((uintptr_t)p & 15) == 0, "vae bind: null or unaligned " + name);
     params_[name] = {(const bf16_t*)p, n};
@@ -183,7 +195,7 @@ class VaeEngine {
     if (gn(s, buf_[cur], buf_[t], h * w, C, "decoder.conv_norm_out", true)) return 1;
     {
       GemmParams g;
-      if (conv_params(g, buf_[t], C, h, w, false, "decoder.conv_out", 3)) return 1;
+      if (conv_params(s, g, buf_[t], C, h, w, false, "decoder.conv_out", 3)) return 1;
       g.out = out;
       g.ldo = 4;
       if (gemm_bf16(g, EPI_STORE_F32, s)) return 1;
@@ -228,8 +240,16 @@ class VaeEngine {
     tH_ = tW_ = 0;
   }
 
-  // pack every 3x3 conv weight [Cout][Cin][3][3] -> [Cout][3][3][Cin_pad]
+  // pack every 3x3 conv weight [Cout][Cin][3][3] -> [Cout][3][3][Cin_pad] (fp8 storage: packed into the bf16
+  // scratch, then quantised)
   int pack_all() {
+    struct Conv {
+      std::string base;
+      const bf16_t* p;
+      int cout, cin, cpad;
+    };
+    std::vector<Conv> convs;
+    long most = 0;
     for (auto& kv : params_) {
       const std::string& n = kv.first;
       if (n.size() < 12 || n.compare(n.size() - 7, 7, ".weight") != 0) continue;
@@ -244,20 +264,44 @@ class VaeEngine {
       FLITE_REQUIRE(kv.second.n % (9L * cout) == 0, "vae: bad conv weight " + n);
       const int cin = (int)(kv.second.n / (9L * cout));
       const int cpad = (cin + 63) / 64 * 64;
+      convs.push_back({base, kv.second.p, cout, cin, cpad});
+      most = std::max(most, 9L * cout * cpad);
+    }
+    w8_.clear();
+    wscratch_ = nullptr;
+    if (fp8_w_ && alloc((void**)&wscratch_, (size_t)most * 2)) return 1;
+    for (const Conv& c : convs) {
       bf16_t* o = nullptr;
-      if (alloc((void**)&o, (size_t)cout * 9 * cpad * 2)) return 1;
-      if (pack_conv_weight(kv.second.p, o, cout, cin, cpad, 0)) return 1;
-      packed_[base] = {o, cpad};
+      if (fp8_w_) {
+        const int K = 9 * c.cpad;
+        uint8_t *q = nullptr, *sc = nullptr;
+        if (alloc((void**)&q, (size_t)c.cout * K)) return 1;
+        if (alloc((void**)&sc, (size_t)c.cout * (K / 32))) return 1;
+        if (pack_conv_weight(c.p, wscratch_, c.cout, c.cin, c.cpad, 0)) return 1;
+        if (mx_quant_rows_rm(wscratch_, c.cout, K, q, sc, 0)) return 1;
+        w8_[c.base] = {q, sc};
+      } else {
+        if (alloc((void**)&o, (size_t)c.cout * 9 * c.cpad * 2)) return 1;
+        if (pack_conv_weight(c.p, o, c.cout, c.cin, c.cpad, 0)) return 1;
+      }
+      packed_[c.base] = {o, c.cpad};
     }
     FLITE_HIP_CHECK(hipDeviceSynchronize());
     return 0;
   }
 
-  int conv_params(GemmParams& g, const bf16_t* in, int cin, long h, long w, bool up, const std::string& name,
-                  int cout) {
+  int conv_params(hipStream_t s, GemmParams& g, const bf16_t* in, int cin, long h, long w, bool up,
+                  const std::string& name, int cout) {
     auto it = packed_.find(name);
     FLITE_REQUIRE(it != packed_.end(), "vae: unbound conv " + name);
     FLITE_REQUIRE(it->second.second == cin, "vae: channel mismatch for " + name);
+    const bf16_t* wt = it->second.first;
+    if (fp8_w_) {  // expand the stored MXFP8 weight into the scratch (stream-ordered before this conv)
+      const auto q = w8_.find(name);
+      FLITE_REQUIRE(q != w8_.end(), "vae: fp8 weight missing for " + name);
+      if (mx_dequant_rows_rm(q->second.first, q->second.second, cout, 9 * cin, wscratch_, s)) return 1;
+      wt = wscratch_;
+    }
     g.conv_in = in;
     g.conv_c = cin;
     g.conv_ih = (int)h;
@@ -266,7 +310,7 @@ class VaeEngine {
     g.conv_ow = (int)(up ? 2 * w : w);
     g.conv_up = up ? 1 : 0;
     g.conv_in_bytes = h * w * cin * 2;
-    g.W = it->second.first;
+    g.W = wt;
     g.ldw = 9L * cin;
     g.bias = P(name + ".bias");
     g.M = g.conv_oh * g.conv_ow;
@@ -278,7 +322,7 @@ class VaeEngine {
   int conv3(hipStream_t s, const bf16_t* in, int cin, long h, long w, bool up, const std::string& name, int cout,
             bf16_t* out, const bf16_t* resid) {
     GemmParams g;
-    if (conv_params(g, in, cin, h, w, up, name, cout)) return 1;
+    if (conv_params(s, g, in, cin, h, w, up, name, cout)) return 1;
     g.out = out;
     g.ldo = cout;
     g.resid = resid;
@@ -394,6 +438,9 @@ class VaeEngine {
   float* S_ = nullptr;
   bf16_t* P_ = nullptr;
   bf16_t* vt_ = nullptr;
+  bool fp8_w_ = false;
+  std::map<std::string, std::pair<uint8_t*, uint8_t*>> w8_;  // fp8 storage: e4m3 bytes, scales [cout][K/32]
+  bf16_t* wscratch_ = nullptr;                                // the expanded weight of the running conv
   double* stats_ = nullptr;
   float* out32_ = nullptr;
   // tiled decode: latent size, tile geometry, tile origins, decoded fp32 tiles (row-major over the grid)
@@ -434,6 +481,11 @@ int flite_vae_destroy(flite_vae* v) {
 int flite_vae_bind(flite_vae* v, const char* name, const void* ptr, long numel) {
   FLITE_REQUIRE(v && name, "flite_vae_bind: null argument");
   return v->eng->bind(name, ptr, numel);
+}
+
+int flite_vae_enable_fp8_weights(flite_vae* v, int on) {
+  FLITE_REQUIRE(v, "flite_vae_enable_fp8_weights: null engine");
+  return v->eng->enable_fp8_weights(on != 0);
 }
 
 int flite_vae_prepare(flite_vae* v, int latent_h, int latent_w) {

@@ -85,6 +85,7 @@ SIGNATURES = {
     "flite_vae_destroy": (_i, [_vp]),
     "flite_vae_bind": (_i, [_vp, _cp, _vp, _l]),
     "flite_vae_prepare": (_i, [_vp, _i, _i]),
+    "flite_vae_enable_fp8_weights": (_i, [_vp, _i]),
     "flite_vae_decode_uint8": (_i, [_vp, _vp, _vp, _i, _vp, _f, _f]),
     "flite_vae_prepare_tiled": (_i, [_vp, _i, _i, _i, _i, _f]),
     "flite_vae_decode_tiled_uint8": (_i, [_vp, _vp, _vp, _i, _vp, _f, _f]),
@@ -561,6 +562,10 @@ class VaeEngine:
 
     def prepare(self, h, w):
         check(self.lib.flite_vae_prepare(self.h, h, w), "flite_vae_prepare")
+
+    def enable_fp8_weights(self, on: bool = True):
+        """MXFP8 storage of the packed conv weights (expanded to bf16 per conv); takes effect at the next prepare."""
+        check(self.lib.flite_vae_enable_fp8_weights(self.h, int(bool(on))), "flite_vae_enable_fp8_weights")
 
     def decode_uint8(self, z, img, scaling, shift):
         require_gpu(z, "latents", torch.float32)

@@ -144,6 +144,7 @@ class AutoencoderKL(nn.Module):
         self.tile_sample_min_size = int(c["sample_size"])
         self.tile_latent_min_size = int(c["sample_size"]) >> (len(c["block_out_channels"]) - 1)
         self.tile_overlap_factor = 0.25
+        self.fp8_weights = False  # enable_layerwise_casting(torch.float8_e4m3fn)
 
     def enable_tiling(self, use_tiling: bool = True):
         """diffusers AutoencoderKL.enable_tiling (the reference calls it at generate.py:78)."""
@@ -159,6 +160,22 @@ class AutoencoderKL(nn.Module):
 
     def disable_slicing(self):
         self.use_slicing = False
+
+    def enable_layerwise_casting(self, storage_dtype=torch.float8_e4m3fn, compute_dtype=torch.bfloat16, **_):
+        """diffusers ModelMixin.enable_layerwise_casting for the decoder (the "fp8 VAE" of SURVEY 8f rank 4): the
+        3x3 conv weights are stored in fp8 and up-cast to bf16 right before each conv. Stored as MXFP8 (e4m3 with
+        one power-of-two scale per 32 input-channel values of a tap) rather than a per-tensor cast (random-init
+        Flux VAE: 34.7 dB from the bf16-weight decode, 50.4 dB from the oracle on the same quantised weights). Norm, attention and bias parameters stay bf16, as diffusers
+        skips them by default."""
+        if storage_dtype not in (torch.float8_e4m3fn, torch.bfloat16):
+            raise _native.FliteError(f"layerwise casting: storage dtype {storage_dtype} is not supported")
+        if compute_dtype != torch.bfloat16:
+            raise _native.FliteError("layerwise casting: the native decoder computes in bf16")
+        self.fp8_weights = storage_dtype == torch.float8_e4m3fn
+        self._prepared = None
+
+    def disable_layerwise_casting(self):
+        self.enable_layerwise_casting(torch.bfloat16)
 
     @classmethod
     def empty(cls, device="cuda", dtype=torch.bfloat16, **cfg):
@@ -222,6 +239,8 @@ class AutoencoderKL(nn.Module):
                 self._engine.bind(n, p.data)
             self._bound = sig
             self._prepared = None
+        if self._prepared is None:
+            self._engine.enable_fp8_weights(self.fp8_weights)
         return self._engine
 
     @torch.no_grad()

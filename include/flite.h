@@ -305,6 +305,10 @@ int flite_vae_create(const flite_vae_config* cfg, flite_vae** out);
 int flite_vae_destroy(flite_vae* vae);
 int flite_vae_bind(flite_vae* vae, const char* name, const void* ptr, long numel);
 /* Workspace + packed conv weights for latents of [latent_channels, latent_h, latent_w]. */
+/* fp8 weight storage (diffusers' layerwise casting with an fp8 storage dtype, compute bf16; no reference
+ * counterpart: SURVEY 8f rank 4): the packed 3x3 conv weights are kept as MXFP8 (e4m3 + one E8M0 scale per 32
+ * input-channel values of a tap) and expanded to bf16 right before each conv. Takes effect at the next prepare. */
+int flite_vae_enable_fp8_weights(flite_vae* vae, int on);
 int flite_vae_prepare(flite_vae* vae, int latent_h, int latent_w);
 /* latents fp32 [n_img, C, h, w] -> images uint8 [n_img, 8h, 8w, 3] (device), decoding z/scaling + shift. */
 int flite_vae_decode_uint8(flite_vae* vae, void* stream, const float* latents, int n_img, void* images,

@@ -79,6 +79,38 @@ def test_vae_decode_uint8(lh, lw):
     assert p >= 40.0
 
 
+def _mx_conv_weight(w):
+    """Fake-quantise a [Cout, Cin, 3, 3] weight the way the engine stores it: packed [Cout][ky][kx][Cin_pad64],
+    MXFP8 per 32 along that row (blocks never straddle a tap since Cin_pad is a multiple of 64)."""
+    cout, cin = w.shape[:2]
+    cpad = (cin + 63) // 64 * 64
+    t = F.pad(w.permute(0, 2, 3, 1), (0, cpad - cin)).reshape(cout, 9 * cpad)
+    t = R.mx_quant(t).reshape(cout, 3, 3, cpad)[..., :cin]
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+# fp8 VAE (SURVEY 8f rank 4; diffusers enable_layerwise_casting with an fp8 storage dtype): the 3x3 conv weights
+# are stored as MXFP8 and expanded to bf16 per conv. Parity target: the fp32 oracle decoder run on the same
+# fake-quantised weights (>= 40 dB, the bar of the bf16 decode); the distance to the bf16-weight decode is the
+# quantisation cost, reported.
+def test_vae_decode_fp8_weights():
+    vae = AutoencoderKL.random(seed=0)
+    sd = make_vae_state_dict(seed=0)
+    sdq = {k: (_mx_conv_weight(v) if v.dim() == 4 and v.shape[-1] == 3 else v) for k, v in sd.items()}
+    lat = torch.randn(1, 16, 8, 8, generator=torch.Generator().manual_seed(11))
+    bf = vae.decode_to_uint8(lat.to(DEV))
+    vae.enable_layerwise_casting(torch.float8_e4m3fn, torch.bfloat16)
+    img = vae.decode_to_uint8(lat.to(DEV))
+    assert torch.equal(img, vae.decode_to_uint8(lat.to(DEV)))
+    p = R.psnr(img.float().cpu(), decode_to_uint8(RefVAEDecoder(sdq), lat).float(), peak=255.0)
+    cost = R.psnr(img.float().cpu(), bf.float().cpu(), peak=255.0)
+    print(f"VAE fp8 weights 8x8: {p:.2f} dB vs the oracle on MX-quantised weights, {cost:.2f} dB vs bf16 weights")
+    assert p >= 40.0
+    assert not torch.equal(img, bf)
+    vae.disable_layerwise_casting()
+    assert torch.equal(vae.decode_to_uint8(lat.to(DEV)), bf)
+
+
 # Tiled decode (diffusers AutoencoderKL.tiled_decode, on in the reference via generate.py:77-78) against the oracle
 # restatement, at a reduced tile size so the oracle stays cheap: tile_latent 16 (128 px), stride 12, 32-px blends,
 # 96-px crops; 20 x 28 latents give a 2 x 3 grid with 8-row and 4-column edge tiles.
