@@ -161,20 +161,20 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
   const int q_len = p.cu_q[b + 1] - q_start;
   if (q0 >= q_len) return;  // uniform over the workgroup (and over all chunks of a pair)
   const int k_start = p.cu_k[b];
-  const int k_len = p.cu_k[b + 1] - k_start;
+  const int k_len = (p.k_end ? p.k_end[b] : p.cu_k[b + 1]) - k_start;
 
   const int lq = lane & 31;
   const int hh = lane >> 5;
   const int q_row = q0 + wave * 32 + lq;  // this lane's query (within the sequence)
 
-  if (k_len <= 0) {  // no keys: output zeros (one chunk writes them)
+  if (k_len <= 0 && p.part_mode == 0) {  // no keys: output zeros (one chunk writes them)
     if (chunk <= 0 && q_row < q_len) {
       bf16_t* o = p.o + (long)(q_start + q_row) * p.o_row_stride + (long)h * p.o_head_stride;
       for (int d = hh * 128; d < hh * 128 + 128; d += 4) *(u32x2*)(o + d) = u32x2{0u, 0u};
     }
     return;
   }
-  const int ntiles_all = (k_len + KT - 1) / KT;
+  const int ntiles_all = k_len > 0 ? (k_len + KT - 1) / KT : 0;  // 0: a partial mode with no keys here
   int t_begin = 0, t_end = ntiles_all;
   if (chunk >= 0) {
     const int per = (ntiles_all + p.n_split - 1) / p.n_split;
@@ -604,6 +604,34 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
   }
 
   if (q_row >= q_len) return;  // lanes l and l + 32 hold the same row: the pairs below stay whole
+  if constexpr (BOUNDED) {
+    if (p.part_mode != 0) {  // partial (O, l) of a disjoint key set: lane (row, hh) holds O columns as below
+      const long prow = (long)(q_start + q_row) * p.H + h;
+      float* po = p.part_o + prow * HD + 4 * hh;
+      if (p.part_mode == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            *(f32x4*)(po + i * 32 + 8 * r4) =
+                f32x4{o_acc[i][4 * r4], o_acc[i][4 * r4 + 1], o_acc[i][4 * r4 + 2], o_acc[i][4 * r4 + 3]};
+        if (hh == 0) p.part_l[prow] = l_run;
+        return;
+      }
+      f32x4 add[8][4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) add[i][r4] = *(const f32x4*)(po + i * 32 + 8 * r4);
+      l_run += p.part_l[prow];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o_acc[i][4 * r4 + e] += add[i][r4][e];
+    }
+  }
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
   bf16_t* orow = p.o + (long)(q_start + q_row) * p.o_row_stride + (long)h * p.o_head_stride;
   // Lane (row, hh) holds columns i*32 + 8*r4 + 4*hh + 0..3. For each pair (r4, r4 + 1) one v_permlane32_swap per
@@ -666,7 +694,10 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
   q.n_main = (p.max_q + QT - 1) / QT;
   q.n_split = 0;
   const int pairs = p.B * p.H;
-  if (p.max_score > 0.f && p.split_ws != nullptr && p.max_q % QT != 0 && pairs <= (int)(CNT_BYTES / 4) &&
+  FLITE_REQUIRE(p.part_mode == 0 || (p.max_score > 0.f && p.part_o && p.part_l),
+                "attention: partial (O, l) modes need the bounded softmax and both partial buffers");
+  if (p.part_mode == 0 && p.max_score > 0.f && p.split_ws != nullptr && p.max_q % QT != 0 &&
+      pairs <= (int)(CNT_BYTES / 4) &&
       (p.max_k <= 0 || p.max_k >= MIN_SPLIT_KEYS)) {
     const long cap = (p.split_ws_bytes - CNT_BYTES) / SLAB_BYTES / pairs;  // slabs per pair in the workspace
     const int S = (int)std::min<long>(std::min(g_attn_cus / pairs, MAX_SPLIT), cap);

@@ -53,6 +53,9 @@ DitEngine::~DitEngine() {
   if (gstream_) hipStreamDestroy(gstream_);
   if (ev_in_) hipEventDestroy(ev_in_);
   if (ev_out_) hipEventDestroy(ev_out_);
+  if (xstream_) hipStreamDestroy(xstream_);
+  if (ev_kv_) hipEventDestroy(ev_kv_);
+  if (ev_x_) hipEventDestroy(ev_x_);
 }
 
 // Destroy the cached graph once every replay of it has finished (a replay may still be in flight on gstream_).
@@ -75,6 +78,8 @@ void DitEngine::free_ws() {
   x_ = nullptr;
   kv_full_ = nullptr;
   cu_full_ = nullptr;
+  part_o_ = part_l_ = nullptr;
+  kend_loc_ = cu_rem_ = nullptr;
   rope_axes_ = nullptr;
 }
 
@@ -264,6 +269,24 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
     std::vector<int> cuf(B + 1);
     for (int i = 0; i <= B; ++i) cuf[i] = i * T_;
     FLITE_HIP_CHECK(hipMemcpy(cu_full_, cuf.data(), (B + 1) * 4, hipMemcpyHostToDevice));
+    // overlapped exchange: local keys [b*Tl, b*Tl + v) of the rank's own rows, remote keys packed per sequence
+    const int v = std::max(0, std::min(T_, (sp_rank_ + 1) * Tl_) - sp_rank_ * Tl_);
+    std::vector<int> kend(B), cur(B + 1);
+    for (int i = 0; i < B; ++i) kend[i] = i * Tl_ + v;
+    for (int i = 0; i <= B; ++i) cur[i] = i * (T_ - v);
+    if (alloc((void**)&part_o_, M_ * D * 4)) return 1;
+    if (alloc((void**)&part_l_, M_ * H * 4)) return 1;
+    if (alloc((void**)&kend_loc_, B * 4)) return 1;
+    if (alloc((void**)&cu_rem_, (B + 1) * 4)) return 1;
+    FLITE_HIP_CHECK(hipMemcpy(kend_loc_, kend.data(), B * 4, hipMemcpyHostToDevice));
+    FLITE_HIP_CHECK(hipMemcpy(cu_rem_, cur.data(), (B + 1) * 4, hipMemcpyHostToDevice));
+    if (!xstream_) {
+      FLITE_HIP_CHECK(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking));
+      FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_kv_, hipEventDisableTiming));
+      FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_x_, hipEventDisableTiming));
+    }
+    const char* no = getenv("FLITE_SP_NO_OVERLAP");  // A/B switch: gather every key first, one attention
+    sp_overlap_ = !(no && no[0] == '1');
   }
   if (alloc((void**)&inv_freq_, 64 * 4)) return 1;
   if (alloc((void**)&rope_axes_, (long)(1 + Hl / P + Wl / P) * 128 * 4)) return 1;
@@ -507,7 +530,8 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     rn.tokens_per_seq = Tl_;
     if (rope_qknorm(rn, s)) return 1;
   }
-  if (sp_n_ > 1 && sp_gather_kv(s)) return 1;  // every key of the sequence (normed, rotated) on every rank
+  const bool sp_ovl = sp_n_ > 1 && sp_overlap_;
+  if (sp_n_ > 1 && !sp_ovl && sp_gather_kv(s)) return 1;  // every key of the sequence on every rank
   {
     AttnParams a;
     a.q = qkv_;
@@ -530,7 +554,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.split_ws = attn_ws_;
     a.split_ws_bytes = attn_ws_bytes_;
     if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
-    if (attn_fwd(a, s)) return 1;
+    if (sp_ovl ? sp_self_attention(s, a) : attn_fwd(a, s)) return 1;
     if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
   }
   if (resid(obuf_, D, b.proj_w, D, gate_sa)) return 1;
@@ -944,6 +968,58 @@ int DitEngine::sp_gather_kv(hipStream_t s) {
                                      hipMemcpyDeviceToDevice, s));
   }
   return 0;
+}
+
+// Self-attention of this rank's query rows with the K/V exchange overlapped (the ring
+// idea with one all-gather). The K/V rows go to the send buffer, the exchange runs on xstream_ while the
+// attention over the rank's OWN keys runs on s, leaving the partial (O, l) in fp32; then the other ranks' rows
+// are packed per sequence (rank order, own block skipped) and a second launch over them adds the partial and
+// normalises. The bounded softmax has a fixed shift, so the two partial sums add exactly as one pass would
+// (up to fp32 summation order). `a` is the whole-sequence parameter set of run_block.
+int DitEngine::sp_self_attention(hipStream_t s, AttnParams a) {
+  const size_t row = 2 * (size_t)D * 2;
+  FLITE_HIP_CHECK(hipMemcpy2DAsync(sp_kv_send_, row, qkv_ + D, 3 * (size_t)D * 2, row, M_, hipMemcpyDeviceToDevice, s));
+  FLITE_HIP_CHECK(hipEventRecord(ev_kv_, s));
+  // (1) own keys, straight from the qkv rows (the last rank's padding rows excluded by k_end)
+  AttnParams l = a;
+  l.k = qkv_ + D;
+  l.v = qkv_ + 2L * D;
+  l.k_row_stride = l.v_row_stride = 3L * D;
+  l.cu_k = cu_self_;
+  l.k_end = kend_loc_;
+  l.max_k = Tl_;
+  l.part_mode = 1;
+  l.part_o = part_o_;
+  l.part_l = part_l_;
+  if (attn_fwd(l, s)) return 1;
+  // (2) the exchange, on the side stream (an RCCL all-gather returns at once; a host-staged one blocks here
+  // while (1) runs)
+  FLITE_HIP_CHECK(hipStreamWaitEvent(xstream_, ev_kv_, 0));
+  FLITE_REQUIRE(sp_fn_(sp_user_, 0, (void*)xstream_) == 0, "sequence parallel: K/V exchange failed");
+  FLITE_HIP_CHECK(hipEventRecord(ev_x_, xstream_));
+  FLITE_HIP_CHECK(hipStreamWaitEvent(s, ev_x_, 0));
+  // (3) the other ranks' rows, packed per sequence: [B][T - v][2D]
+  const int v = std::max(0, std::min(T_, (sp_rank_ + 1) * Tl_) - sp_rank_ * Tl_);
+  const long rem = T_ - v;
+  for (int q = 0; q < sp_n_; ++q) {
+    if (q == sp_rank_) continue;
+    const int valid = std::min(T_, (q + 1) * Tl_) - q * Tl_;
+    if (valid <= 0) continue;
+    const long off = (long)q * Tl_ - (q > sp_rank_ ? v : 0);
+    FLITE_HIP_CHECK(hipMemcpy2DAsync(kv_full_ + off * 2 * D, (size_t)rem * row, sp_kv_recv_ + (long)q * M_ * 2 * D,
+                                     (size_t)Tl_ * row, (size_t)valid * row, B_, hipMemcpyDeviceToDevice, s));
+  }
+  // (4) remote keys, adding the partial of (1)
+  AttnParams r = a;
+  r.k = kv_full_;
+  r.v = kv_full_ + D;
+  r.k_row_stride = r.v_row_stride = 2L * D;
+  r.cu_k = cu_rem_;
+  r.max_k = (int)rem;
+  r.part_mode = 2;
+  r.part_o = part_o_;
+  r.part_l = part_l_;
+  return attn_fwd(r, s);
 }
 
 // final-projection rows of every rank -> the model output [B][HW][C p p] (fout_), registers and padding dropped

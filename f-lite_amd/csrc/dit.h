@@ -73,6 +73,7 @@ class DitEngine {
 
   int run_block(hipStream_t s, int blk, const float* mod, long mseg);
   int sp_gather_kv(hipStream_t s);
+  int sp_self_attention(hipStream_t s, AttnParams a);
   int sp_gather_out(hipStream_t s);
   int run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg);
   int alloc_fp8_act();
@@ -95,6 +96,13 @@ class DitEngine {
   bf16_t *sp_kv_send_ = nullptr, *sp_kv_recv_ = nullptr, *kv_full_ = nullptr;
   float *sp_out_send_ = nullptr, *sp_out_recv_ = nullptr;
   int *cu_full_ = nullptr;
+  // overlapped exchange (sp_self_attention): partial (O, l) of the local keys, the local key-range ends, the
+  // remote keys' cu_seqlens, and the side stream the K/V all-gather runs on
+  float *part_o_ = nullptr, *part_l_ = nullptr;
+  int *kend_loc_ = nullptr, *cu_rem_ = nullptr;
+  hipStream_t xstream_ = nullptr;
+  hipEvent_t ev_kv_ = nullptr, ev_x_ = nullptr;
+  bool sp_overlap_ = true;
   long M_ = 0;
   int nctx_ = 0, nseq_ctx_ = 0, ctx_max_len_ = 0;
   // workspace

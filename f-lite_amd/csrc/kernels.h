@@ -75,6 +75,15 @@ struct AttnParams {
   // left zeroed by every launch; launches sharing it must be stream-ordered
   void* split_ws = nullptr;
   long split_ws_bytes = 0;
+  // optional key-range ends (device int32 [B]); null: cu_k[b + 1]
+  const int* k_end = nullptr;
+  // Partial (O, l) hand-over between two launches over disjoint key sets of the same queries (bounded softmax
+  // only: with the fixed shift the two partial sums add without rescaling; the sequence-parallel overlap).
+  // 1: write the unnormalised O (fp32, [query row][H * 256]) and the row sums l ([query row][H]) instead of o;
+  // 2: add them to this launch's O and l, then normalise into o. No tail split in either mode.
+  int part_mode = 0;
+  float* part_o = nullptr;
+  float* part_l = nullptr;
   int n_main = 0, n_split = 0;  // set by the launcher
   int split_first = 0;          // set by the launcher: tail chunks dispatched before the full q-tiles
 };

@@ -417,7 +417,7 @@ class DitEngine:
     def set_sequence_parallel(self, rank: int = 0, nranks: int = 1, allgather=None):
         """flite_dit_set_sequence_parallel: this engine computes rows [rank*Tl, (rank+1)*Tl) of every sequence.
         allgather(send, recv) must all-gather the uint8 device tensor `send` into `recv` (nranks x, rank order)
-        on the current stream. nranks = 1 switches back to the whole sequence. Call prepare() afterwards."""
+        on the current stream (the engine makes its exchange stream current around the call). nranks = 1 switches back to the whole sequence. Call prepare() afterwards."""
         if nranks > 1:
             if allgather is None:
                 raise FliteError("sequence parallelism needs an allgather(send, recv) exchange")
@@ -425,7 +425,13 @@ class DitEngine:
             def cb(user, which, stream):
                 try:
                     send, recv = self._sp_bufs[which]
-                    allgather(send, recv)
+                    # the engine names the stream the exchange belongs on (a side stream for the K/V rows,
+                    # overlapped with the attention over the rank's own keys)
+                    if stream:
+                        with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=send.device)):
+                            allgather(send, recv)
+                    else:  # the null stream
+                        allgather(send, recv)
                     return 0
                 except Exception as e:  # reported by the failing flite call
                     self._sp_error = e

@@ -7,6 +7,10 @@ loop (flite_dit_sample, eager) is (within 3 dB, and >= 35 dB), whose GEMMs and a
 (other tile / split choices); on the tiny model also >= 50 dB from that loop. N = 3 leaves padding rows on
 the last rank (T = 80 and 1040 are not multiples of 3). The 512^2 case runs the 10B layout (cross-attention in every block) at depth 2 with 1040-key sequences,
 so the gathered keys take the attention kernel's multi-tile and tail-split paths.
+
+By default the K/V exchange overlaps the attention over each rank's own keys (a partial (O, l) launch, then
+one over the other ranks' keys that adds it: dit.cpp sp_self_attention); `overlap=False` runs the gather-first
+path (FLITE_SP_NO_OVERLAP=1), one attention over every key.
 """
 import os
 import socket
@@ -51,8 +55,10 @@ def _inputs(case):
     return lat, pos, neg
 
 
-def _worker(rank, world, port, case, q):
+def _worker(rank, world, port, case, q, overlap=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    if not overlap:
+        os.environ["FLITE_SP_NO_OVERLAP"] = "1"
     try:
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -83,11 +89,11 @@ def _worker(rank, world, port, case, q):
         q.put((rank, repr(e)))
 
 
-def _run(case, world):
+def _run(case, world, overlap=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -113,15 +119,18 @@ def _batched(case):
                             use_graph=False).images.float().cpu()
 
 
-@pytest.mark.parametrize("case,world", [("tiny", 2), ("tiny", 3), ("10b_d2_512", 2), ("10b_d2_512", 3)])
-def test_sequence_parallel_matches_whole_sequence_loop(case, world):
-    res = _run(case, world)
+@pytest.mark.parametrize("case,world,overlap", [("tiny", 2, True), ("tiny", 3, True), ("10b_d2_512", 2, True),
+                                                ("10b_d2_512", 3, True), ("tiny", 3, False),
+                                                ("10b_d2_512", 3, False)])
+def test_sequence_parallel_matches_whole_sequence_loop(case, world, overlap):
+    res = _run(case, world, overlap)
     got = res[0][0]
     for r in range(1, world):
         assert torch.equal(res[r][0], got), f"rank {r} differs from rank 0"
     batched = _batched(case)
     p_b = R.psnr(got, batched)
-    msg = f"sequence-parallel x{world} ({case}): {p_b:.2f} dB vs the whole-sequence loop"
+    msg = f"sequence-parallel x{world} ({case}, {'overlapped' if overlap else 'gather-first'}): {p_b:.2f} dB " \
+          "vs the whole-sequence loop"
     lat, pos, neg = _inputs(case)
     import dataclasses
 
