@@ -25,6 +25,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "fp8.h"
 #include "kernels.h"
 
 namespace flite {
@@ -599,6 +600,43 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         st.y = pack2bf(acc[2] * inv, acc[3] * inv);
         *(u32x2*)(p.o + (long)(q_start + row) * p.o_row_stride + (long)h * p.o_head_stride + d) = st;
       }
+      if (p.o8) {  // the tail rows' MXFP8 copy, from the bf16 rows this workgroup just stored
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int rows = min(q_len - q0, 32 * n_live);
+        for (int t = tid; t < rows * 8; t += NT) {
+          const int row = q0 + (t >> 3), i = t & 7;
+          const long grow = q_start + row;
+          const u32x4* src = (const u32x4*)(p.o + grow * p.o_row_stride + (long)h * p.o_head_stride + i * 32);
+          float x[32];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const u32x4 w = src[q];
+            const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              x[8 * q + 2 * j] = __uint_as_float(ws[j] << 16);
+              x[8 * q + 2 * j + 1] = __uint_as_float(ws[j] & 0xffff0000u);
+            }
+          }
+          float amax = 0.f;
+#pragma unroll
+          for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(x[j]));
+          const int e = mx_exp(amax);
+          const float is = mx_inv(e);
+          u32x4 o[2];
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf)
+            o[hf] = u32x4{pack4_fp8(x + 16 * hf, is), pack4_fp8(x + 16 * hf + 4, is), pack4_fp8(x + 16 * hf + 8, is),
+                          pack4_fp8(x + 16 * hf + 12, is)};
+          u32x4* dst = (u32x4*)(p.o8 + grow * p.o_row_stride + (long)h * p.o_head_stride + i * 32);
+          dst[0] = o[0];
+          dst[1] = o[1];
+          const long kb = (long)h * (HD / 32) + i;
+          p.o8_scale[((kb >> 2) * p.o8_rows_pad + grow) * 4 + (kb & 3)] = (uint8_t)(e + 127);
+        }
+      }
       return;
     }
   }
@@ -633,6 +671,38 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     }
   }
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  if (p.o8) {  // MXFP8 straight from the accumulators: 32-column block i = this lane's 16 values + lane ^ 32's
+    const long grow = q_start + q_row;
+    uint8_t* o8row = p.o8 + grow * p.o_row_stride + (long)h * p.o_head_stride;
+    unsigned sc_lo = 0, sc_hi = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float x[16];
+      float amax = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        x[r] = bf2f(f2bf(o_acc[i][r] * inv));  // the bf16 value quant_rows_fp8 would have read
+        amax = fmaxf(amax, fabsf(x[r]));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+      const int e = mx_exp(amax);
+      const float is = mx_inv(e);
+      unsigned d[4];
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) d[r4] = pack4_fp8(x + 4 * r4, is);  // columns 8 r4 + 4 hh + 0..3
+#pragma unroll
+      for (int rp = 0; rp < 2; ++rp) {  // lower half: columns 16 rp + 0..7, upper: 16 rp + 8..15
+        const auto w = __builtin_amdgcn_permlane32_swap(d[2 * rp], d[2 * rp + 1], false, false);
+        *(u32x2*)(o8row + i * 32 + 16 * rp + 8 * hh) = u32x2{w[0], w[1]};
+      }
+      const unsigned byte = (unsigned)(e + 127) << (8 * (i & 3));
+      if (i < 4) sc_lo |= byte; else sc_hi |= byte;
+    }
+    // the row's 8 block scales of this head = two 128-deep k-tiles: [k-tile][row][4] words
+    const long kt = (long)h * (HD / 128) + hh;
+    *(unsigned*)(p.o8_scale + (kt * p.o8_rows_pad + grow) * 4) = hh ? sc_hi : sc_lo;
+    return;
+  }
   bf16_t* orow = p.o + (long)(q_start + q_row) * p.o_row_stride + (long)h * p.o_head_stride;
   // Lane (row, hh) holds columns i*32 + 8*r4 + 4*hh + 0..3. For each pair (r4, r4 + 1) one v_permlane32_swap per
   // dword gives the lower half-wave columns 16*rp + 0..7 and the upper half 16*rp + 8..15: one 16-B store per
@@ -696,6 +766,9 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
   const int pairs = p.B * p.H;
   FLITE_REQUIRE(p.part_mode == 0 || (p.max_score > 0.f && p.part_o && p.part_l),
                 "attention: partial (O, l) modes need the bounded softmax and both partial buffers");
+  FLITE_REQUIRE(!p.o8 || (p.o8_scale && p.part_mode != 1 && p.o_row_stride % 128 == 0 && p.o_head_stride == HD &&
+                          p.o8_rows_pad > 0),
+                "attention: MXFP8 output needs scales, 128-aligned rows and whole heads");
   if (p.part_mode == 0 && p.max_score > 0.f && p.split_ws != nullptr && p.max_q % QT != 0 &&
       pairs <= (int)(CNT_BYTES / 4) &&
       (p.max_k <= 0 || p.max_k >= MIN_SPLIT_KEYS)) {

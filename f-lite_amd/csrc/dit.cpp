@@ -656,6 +656,10 @@ int DitEngine::enable_fp8(hipStream_t s, bool on) {
     return 0;
   }
   FLITE_REQUIRE(sp_n_ == 1, "enable_fp8: not with sequence parallelism");
+  {
+    const char* un = getenv("FLITE_FP8_ATTN_UNFUSED");  // A/B switch: bf16 attention output + quant_rows_fp8
+    attn_mx_ = !(un && un[0] == '1');
+  }
   if (check_bound()) return 2;
   FLITE_REQUIRE(D % 128 == 0 && F % 128 == 0, "fp8: hidden and MLP widths must be multiples of 128");
   if (w8_.empty()) {
@@ -774,6 +778,11 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     a.max_score = kQKNormScoreBound;
     a.split_ws = attn_ws_;
     a.split_ws_bytes = attn_ws_bytes_;
+    if (attn_mx_) {  // the proj GEMM's MXFP8 A operand straight from the attention epilogue
+      a.o8 = obuf8_;
+      a.o8_scale = obuf8_s_;
+      a.o8_rows_pad = mpad_;
+    }
     return attn_fwd(a, s);
   };
   auto qk_norm = [&](long ldx, int heads, int rope_heads) -> int {
@@ -802,7 +811,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
   if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, Tl_)) return 1;
   if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
-  if (quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
+  if (!attn_mx_ && quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
   if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa)) return 1;
   // --- cross attention ---
   if (b.cross) {
@@ -812,7 +821,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
       return 1;
     if (!fused && qk_norm(D, H, 0)) return 1;
     if (attn(qkv_, D, ctx_kv_[blk], ctx_kv_[blk] + D, 2L * D, cu_ctx_, ctx_max_len_)) return 1;
-    if (quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
+    if (!attn_mx_ && quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
     if (g8(obuf8_, obuf8_s_, q.cproj, q.cproj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_ca)) return 1;
   }
   // --- SwiGLU MLP ---

@@ -103,6 +103,7 @@ class DitEngine {
   hipStream_t xstream_ = nullptr;
   hipEvent_t ev_kv_ = nullptr, ev_x_ = nullptr;
   bool sp_overlap_ = true;
+  bool attn_mx_ = true;  // fp8 path: the attention writes the proj GEMM's MXFP8 operand itself
   long M_ = 0;
   int nctx_ = 0, nseq_ctx_ = 0, ctx_max_len_ = 0;
   // workspace

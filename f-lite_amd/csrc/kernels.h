@@ -84,6 +84,12 @@ struct AttnParams {
   int part_mode = 0;
   float* part_o = nullptr;
   float* part_l = nullptr;
+  // Optional MXFP8 output (the fp8 DiT's proj A operand, bound for fp8.hip's layout): o8 e4m3 bytes at the
+  // element offsets of o, scales [cols/128][o8_rows_pad][4] by query row. The values are the bf16 outputs
+  // quantised (bit-identical to quant_rows_fp8 of o). The tail-split rows still pass through o (bf16).
+  uint8_t* o8 = nullptr;
+  uint8_t* o8_scale = nullptr;
+  long o8_rows_pad = 0;
   int n_main = 0, n_split = 0;  // set by the launcher
   int split_first = 0;          // set by the launcher: tail chunks dispatched before the full q-tiles
 };

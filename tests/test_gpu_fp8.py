@@ -209,3 +209,25 @@ def test_10b_fp8_full_size_forward():
     p = psnr(f8, bf)
     print(f"10B 1344x896 full-depth forward: fp8 vs bf16 path {p:.2f} dB")
     assert p > 15.0
+
+
+@pytest.mark.parametrize("preset,hw", [("tiny", (16, 16)), ("10b_d2", (112, 168))])
+def test_fp8_attention_mx_output_matches_quant_rows(monkeypatch, preset, hw):
+    """The fp8 path's attention writes the proj GEMM's MXFP8 operand itself (attention.hip, AttnParams.o8):
+    bit-identical to the bf16 attention output + quant_rows_fp8 (FLITE_FP8_ATTN_UNFUSED=1). The 10B-layout case
+    (depth 2, 1344x896: T = 4720, 112-row tails) also covers the tail-split rows, quantised after the reduce."""
+    cfg = dict(PRESETS["10b"], depth=2) if preset == "10b_d2" else PRESETS[preset]
+    m = DiT.random(seed=0, device=DEV, **cfg)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 16, *hw, generator=g).bfloat16().to(DEV)
+    ctx = torch.randn(2, 64, cfg["cross_attn_input_size"], generator=g).bfloat16().to(DEV)
+    t = torch.tensor([0.6, 0.6]).bfloat16().to(DEV)
+    monkeypatch.setenv("FLITE_FP8_ATTN_UNFUSED", "1")
+    m.enable_fp8(True)
+    unfused = m(x, ctx, None, t, output_dtype=torch.float32).cpu()
+    m.enable_fp8(False)
+    monkeypatch.delenv("FLITE_FP8_ATTN_UNFUSED")
+    m.enable_fp8(True)
+    fused = m(x, ctx, None, t, output_dtype=torch.float32).cpu()
+    assert torch.isfinite(fused).all()
+    assert torch.equal(fused, unfused)
