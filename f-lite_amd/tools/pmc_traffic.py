@@ -25,7 +25,7 @@ from collections import defaultdict
 
 # probe name -> substring of the (demangled) kernel name that identifies it uniquely
 KERNELS = {
-    "gateup": "gemm_bf16_kernel<3, false>",  # EPI_SWIGLU_BF16, dense operands
+    "gateup": "gemm_bf16_kernel<3, false,",  # EPI_SWIGLU_BF16, dense operands (any tile height)
 }
 N_SIMD = 256 * 4
 N_XCD = 8
