@@ -668,6 +668,16 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         for (int r4 = 0; r4 < 4; ++r4)
 #pragma unroll
           for (int e = 0; e < 4; ++e) o_acc[i][4 * r4 + e] += add[i][r4][e];
+      if (p.part_mode == 3) {  // ring step: the sum stays a partial for the next key block
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            *(f32x4*)(po + i * 32 + 8 * r4) =
+                f32x4{o_acc[i][4 * r4], o_acc[i][4 * r4 + 1], o_acc[i][4 * r4 + 2], o_acc[i][4 * r4 + 3]};
+        if (hh == 0) p.part_l[prow] = l_run;
+        return;
+      }
     }
   }
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
@@ -766,7 +776,9 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
   const int pairs = p.B * p.H;
   FLITE_REQUIRE(p.part_mode == 0 || (p.max_score > 0.f && p.part_o && p.part_l),
                 "attention: partial (O, l) modes need the bounded softmax and both partial buffers");
-  FLITE_REQUIRE(!p.o8 || (p.o8_scale && p.part_mode != 1 && p.o_row_stride % 128 == 0 && p.o_head_stride == HD &&
+  FLITE_REQUIRE(p.part_mode >= 0 && p.part_mode <= 3, "attention: part_mode is 0 (whole), 1 (write partial), "
+                "2 (add partial, normalise) or 3 (add partial, write partial)");
+  FLITE_REQUIRE(!p.o8 || (p.o8_scale && (p.part_mode == 0 || p.part_mode == 2) && p.o_row_stride % 128 == 0 && p.o_head_stride == HD &&
                           p.o8_rows_pad > 0),
                 "attention: MXFP8 output needs scales, 128-aligned rows and whole heads");
   if (p.part_mode == 0 && p.max_score > 0.f && p.split_ws != nullptr && p.max_q % QT != 0 &&

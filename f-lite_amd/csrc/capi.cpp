@@ -217,6 +217,11 @@ int flite_dit_sp_bind_buffers(flite_dit* dit, void* kv_send, void* kv_recv, void
   return dit->eng->sp_bind_buffers(kv_send, kv_recv, out_send, out_recv);
 }
 
+int flite_dit_sp_set_ring(flite_dit* dit, int ring) {
+  FLITE_REQUIRE(dit != nullptr, "flite_dit_sp_set_ring: null engine");
+  return dit->eng->set_sp_ring(ring);
+}
+
 int flite_dit_destroy(flite_dit* dit) {
   if (dit) {
     delete dit->eng;

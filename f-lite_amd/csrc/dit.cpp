@@ -56,6 +56,10 @@ DitEngine::~DitEngine() {
   if (xstream_) hipStreamDestroy(xstream_);
   if (ev_kv_) hipEventDestroy(ev_kv_);
   if (ev_x_) hipEventDestroy(ev_x_);
+  for (int i = 0; i < 2; ++i) {
+    if (ev_ring_[i]) hipEventDestroy(ev_ring_[i]);
+    if (ev_used_[i]) hipEventDestroy(ev_used_[i]);
+  }
 }
 
 // Destroy the cached graph once every replay of it has finished (a replay may still be in flight on gstream_).
@@ -79,7 +83,7 @@ void DitEngine::free_ws() {
   kv_full_ = nullptr;
   cu_full_ = nullptr;
   part_o_ = part_l_ = nullptr;
-  kend_loc_ = cu_rem_ = nullptr;
+  kend_loc_ = cu_rem_ = kend_all_ = nullptr;
   rope_axes_ = nullptr;
 }
 
@@ -280,10 +284,19 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
     if (alloc((void**)&cu_rem_, (B + 1) * 4)) return 1;
     FLITE_HIP_CHECK(hipMemcpy(kend_loc_, kend.data(), B * 4, hipMemcpyHostToDevice));
     FLITE_HIP_CHECK(hipMemcpy(cu_rem_, cur.data(), (B + 1) * 4, hipMemcpyHostToDevice));
+    std::vector<int> ka((size_t)sp_n_ * B);
+    for (int q = 0; q < sp_n_; ++q)
+      for (int i = 0; i < B; ++i) ka[(size_t)q * B + i] = i * Tl_ + std::max(0, std::min(T_, (q + 1) * Tl_) - q * Tl_);
+    if (alloc((void**)&kend_all_, (long)sp_n_ * B * 4)) return 1;
+    FLITE_HIP_CHECK(hipMemcpy(kend_all_, ka.data(), (size_t)sp_n_ * B * 4, hipMemcpyHostToDevice));
     if (!xstream_) {
       FLITE_HIP_CHECK(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking));
       FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_kv_, hipEventDisableTiming));
       FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_x_, hipEventDisableTiming));
+      for (int i = 0; i < 2; ++i) {
+        FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_ring_[i], hipEventDisableTiming));
+        FLITE_HIP_CHECK(hipEventCreateWithFlags(&ev_used_[i], hipEventDisableTiming));
+      }
     }
     const char* no = getenv("FLITE_SP_NO_OVERLAP");  // A/B switch: gather every key first, one attention
     sp_overlap_ = !(no && no[0] == '1');
@@ -530,8 +543,10 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     rn.tokens_per_seq = Tl_;
     if (rope_qknorm(rn, s)) return 1;
   }
-  const bool sp_ovl = sp_n_ > 1 && sp_overlap_;
-  if (sp_n_ > 1 && !sp_ovl && sp_gather_kv(s)) return 1;  // every key of the sequence on every rank
+  // the ring needs a key in every rank's block ((N - 1) Tl < T); otherwise the all-gather exchange runs
+  const bool sp_rng = sp_n_ > 1 && sp_ring_ && (long)(sp_n_ - 1) * Tl_ < T_;
+  const bool sp_ovl = sp_n_ > 1 && sp_overlap_ && !sp_rng;
+  if (sp_n_ > 1 && !sp_ovl && !sp_rng && sp_gather_kv(s)) return 1;  // every key of the sequence on every rank
   {
     AttnParams a;
     a.q = qkv_;
@@ -554,7 +569,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.split_ws = attn_ws_;
     a.split_ws_bytes = attn_ws_bytes_;
     if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
-    if (sp_ovl ? sp_self_attention(s, a) : attn_fwd(a, s)) return 1;
+    if (sp_rng ? sp_ring_attention(s, a) : sp_ovl ? sp_self_attention(s, a) : attn_fwd(a, s)) return 1;
     if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
   }
   if (resid(obuf_, D, b.proj_w, D, gate_sa)) return 1;
@@ -1029,6 +1044,67 @@ int DitEngine::sp_self_attention(hipStream_t s, AttnParams a) {
   r.part_o = part_o_;
   r.part_l = part_l_;
   return attn_fwd(r, s);
+}
+
+// Self-attention of this rank's query rows over a ring of K/V blocks (ring attention over T):
+// step 0 attends to the rank's own keys while the first shift (own block -> rank + 1, rank - 1's block -> ring
+// slot 0) runs on xstream_; step j attends to the block of rank (r - j) mod N in slot (j - 1) & 1 while shift j + 1
+// forwards that block and receives the next into the other slot. Every step but the last leaves the unnormalised
+// partial (O, l) (attention part_mode 1 / 3); the last adds it and normalises (part_mode 2). The bounded softmax's
+// fixed shift makes the partials add exactly, so no (m, l) rescale is needed. A slot is overwritten only after the
+// attention that read it (ev_used_). Per step each rank sends and receives one block (2 x Tl x D bf16 per
+// sequence): N - 1 neighbour transfers over one xGMI link each, instead of an all-gather.
+int DitEngine::sp_ring_attention(hipStream_t s, AttnParams a) {
+  const size_t row = 2 * (size_t)D * 2;
+  const int N = sp_n_;
+  bf16_t* slot[2] = {sp_kv_recv_, sp_kv_recv_ + M_ * 2 * D};  // kv_recv holds N >= 2 blocks: two ring slots
+  FLITE_HIP_CHECK(hipMemcpy2DAsync(sp_kv_send_, row, qkv_ + D, 3 * (size_t)D * 2, row, M_, hipMemcpyDeviceToDevice, s));
+  FLITE_HIP_CHECK(hipEventRecord(ev_kv_, s));
+  // shift 1 on the side stream: own block -> rank + 1, rank - 1's block -> slot 0
+  FLITE_HIP_CHECK(hipStreamWaitEvent(xstream_, ev_kv_, 0));
+  FLITE_REQUIRE(sp_fn_(sp_user_, 2, (void*)xstream_) == 0, "sequence parallel: ring shift failed");
+  FLITE_HIP_CHECK(hipEventRecord(ev_ring_[0], xstream_));
+  // step 0: own keys, straight from the qkv rows
+  AttnParams l = a;
+  l.k = qkv_ + D;
+  l.v = qkv_ + 2L * D;
+  l.k_row_stride = l.v_row_stride = 3L * D;
+  l.cu_k = cu_self_;
+  l.k_end = kend_loc_;
+  l.max_k = Tl_;
+  l.part_mode = 1;
+  l.part_o = part_o_;
+  l.part_l = part_l_;
+  if (attn_fwd(l, s)) return 1;
+  for (int j = 1; j < N; ++j) {
+    const int cur = (j - 1) & 1;
+    FLITE_HIP_CHECK(hipStreamWaitEvent(s, ev_ring_[cur], 0));  // block of rank (r - j) mod N has landed
+    if (j + 1 < N) {
+      // shift j + 1: forward the block in `cur`, receive into the other slot once step j - 1 has read it
+      if (j >= 2) FLITE_HIP_CHECK(hipStreamWaitEvent(xstream_, ev_used_[j & 1], 0));
+      FLITE_REQUIRE(sp_fn_(sp_user_, 2 + j, (void*)xstream_) == 0, "sequence parallel: ring shift failed");
+      FLITE_HIP_CHECK(hipEventRecord(ev_ring_[j & 1], xstream_));
+    }
+    const int q = ((sp_rank_ - j) % N + N) % N;
+    AttnParams r = a;
+    r.k = slot[cur];
+    r.v = slot[cur] + D;
+    r.k_row_stride = r.v_row_stride = 2L * D;
+    r.cu_k = cu_self_;
+    r.k_end = kend_all_ + (long)q * B_;
+    r.max_k = Tl_;
+    r.part_mode = j + 1 < N ? 3 : 2;
+    r.part_o = part_o_;
+    r.part_l = part_l_;
+    if (attn_fwd(r, s)) return 1;
+    FLITE_HIP_CHECK(hipEventRecord(ev_used_[cur], s));
+  }
+  return 0;
+}
+
+int DitEngine::set_sp_ring(int on) {
+  sp_ring_ = on != 0;
+  return 0;
 }
 
 // final-projection rows of every rank -> the model output [B][HW][C p p] (fout_), registers and padding dropped

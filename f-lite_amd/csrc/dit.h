@@ -55,6 +55,7 @@ class DitEngine {
   int set_sequence_parallel(int rank, int nranks, flite_sp_allgather_fn fn, void* user);
   int sp_buffer_bytes(long* kv_send, long* out_send) const;
   int sp_bind_buffers(void* kv_send, void* kv_recv, void* out_send, void* out_recv);
+  int set_sp_ring(int on);
 
   const flite_dit_config cfg;
   int D, H, F, R, P, C;
@@ -74,6 +75,7 @@ class DitEngine {
   int run_block(hipStream_t s, int blk, const float* mod, long mseg);
   int sp_gather_kv(hipStream_t s);
   int sp_self_attention(hipStream_t s, AttnParams a);
+  int sp_ring_attention(hipStream_t s, AttnParams a);
   int sp_gather_out(hipStream_t s);
   int run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg);
   int alloc_fp8_act();
@@ -103,6 +105,11 @@ class DitEngine {
   hipStream_t xstream_ = nullptr;
   hipEvent_t ev_kv_ = nullptr, ev_x_ = nullptr;
   bool sp_overlap_ = true;
+  // ring exchange (sp_ring_attention): N - 1 neighbour shifts of one rank's K/V block, each overlapped with the
+  // attention over the block before it; kend_all_[q][b] = key-range end of rank q's block in sequence b
+  bool sp_ring_ = false;
+  int* kend_all_ = nullptr;
+  hipEvent_t ev_ring_[2] = {nullptr, nullptr}, ev_used_[2] = {nullptr, nullptr};
   bool attn_mx_ = true;  // fp8 path: the attention writes the proj GEMM's MXFP8 operand itself
   long M_ = 0;
   int nctx_ = 0, nseq_ctx_ = 0, ctx_max_len_ = 0;

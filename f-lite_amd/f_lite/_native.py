@@ -100,6 +100,7 @@ SIGNATURES = {
     "flite_dit_set_sequence_parallel": (_i, [_vp, _i, _i, _vp, _vp]),
     "flite_dit_sp_buffer_bytes": (_i, [_vp, ctypes.POINTER(_l), ctypes.POINTER(_l)]),
     "flite_dit_sp_bind_buffers": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "flite_dit_sp_set_ring": (_i, [_vp, _i]),
     "flite_dit_set_probe": (_i, [_vp, _i, _i]),
     "flite_dit_read_probe": (_i, [_vp, ctypes.POINTER(_f), _i, ctypes.POINTER(_i)]),
 }
@@ -414,24 +415,36 @@ class DitEngine:
         self._sp_error = None
         self._device = None
 
-    def set_sequence_parallel(self, rank: int = 0, nranks: int = 1, allgather=None):
+    def set_sequence_parallel(self, rank: int = 0, nranks: int = 1, allgather=None, ring_shift=None):
         """flite_dit_set_sequence_parallel: this engine computes rows [rank*Tl, (rank+1)*Tl) of every sequence.
         allgather(send, recv) must all-gather the uint8 device tensor `send` into `recv` (nranks x, rank order)
-        on the current stream (the engine makes its exchange stream current around the call). nranks = 1 switches back to the whole sequence. Call prepare() afterwards."""
+        on the current stream (the engine makes its exchange stream current around the call). With
+        ring_shift(send, recv) given, the self-attention's keys travel as a ring instead (flite_dit_sp_set_ring):
+        ring_shift must send `send` to rank + 1 and receive rank - 1's block into `recv` (same size).
+        nranks = 1 switches back to the whole sequence. Call prepare() afterwards."""
         if nranks > 1:
             if allgather is None:
                 raise FliteError("sequence parallelism needs an allgather(send, recv) exchange")
 
+            def bufs(which):
+                if which < 2:
+                    return self._sp_bufs[which], allgather
+                k = which - 1  # ring shift k = 1 .. N-1 (flite.h: flite_dit_sp_set_ring)
+                (ks, kr), _ = self._sp_bufs
+                n = ks.numel()
+                slot = lambda i: kr[i * n:(i + 1) * n]  # noqa: E731
+                return (ks if k == 1 else slot((k - 2) & 1), slot((k - 1) & 1)), ring_shift
+
             def cb(user, which, stream):
                 try:
-                    send, recv = self._sp_bufs[which]
+                    (send, recv), fn = bufs(which)
                     # the engine names the stream the exchange belongs on (a side stream for the K/V rows,
                     # overlapped with the attention over the rank's own keys)
                     if stream:
                         with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=send.device)):
-                            allgather(send, recv)
+                            fn(send, recv)
                     else:  # the null stream
-                        allgather(send, recv)
+                        fn(send, recv)
                     return 0
                 except Exception as e:  # reported by the failing flite call
                     self._sp_error = e
@@ -446,6 +459,8 @@ class DitEngine:
         self._sp_bufs = None
         check(self.lib.flite_dit_set_sequence_parallel(self.h, rank, nranks, fn, None),
               "flite_dit_set_sequence_parallel")
+        check(self.lib.flite_dit_sp_set_ring(self.h, int(nranks > 1 and ring_shift is not None)),
+              "flite_dit_sp_set_ring")
 
     def __del__(self):
         try:

@@ -156,16 +156,41 @@ def all_gather_rows(send: torch.Tensor, recv: torch.Tensor, group=None) -> None:
         dist.all_gather_into_tensor(recv, send, group=group)
 
 
+def ring_shift_rows(send: torch.Tensor, recv: torch.Tensor, group=None) -> None:
+    """One ring step: send `send` to the next rank of the group and receive the previous rank's block into `recv`
+    (equal sizes). RCCL send/recv over one xGMI link with "nccl"; gloo stages through the host."""
+    import torch.distributed as dist
+
+    n = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    nxt = dist.get_global_rank(group, (r + 1) % n) if group is not None else (r + 1) % n
+    prv = dist.get_global_rank(group, (r - 1) % n) if group is not None else (r - 1) % n
+    if dist.get_backend(group) == "gloo":
+        host = send.cpu()
+        buf = torch.empty_like(host)
+        reqs = [dist.isend(host, nxt, group=group), dist.irecv(buf, prv, group=group)]
+        for q in reqs:
+            q.wait()
+        recv.copy_(buf)
+    else:
+        ops = [dist.P2POp(dist.isend, send, nxt, group), dist.P2POp(dist.irecv, recv, prv, group)]
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+
+
 def sequence_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Tensor,
                              negative_prompt_embeds: Optional[torch.Tensor] = None, num_inference_steps: int = 30,
-                             guidance_scale: float = 6.0, alpha: Optional[float] = None, group=None) -> torch.Tensor:
+                             guidance_scale: float = 6.0, alpha: Optional[float] = None, group=None,
+                             ring: bool = False) -> torch.Tensor:
     """Single-image latency mode over the N ranks of `group`: the denoise loop of
     FLitePipeline.__call__ (pipeline.py:250-297) with every DiT launch split by token rows. Rank r computes rows
     [r*Tl, (r+1)*Tl) of each sequence of the CFG batch (Tl = ceil(T / N)); per block its K/V rows are
     all-gathered (2 x T x D bf16 per sequence), per step the output rows. Every rank ends each step with the
     full model output and applies the same native CFG + Euler update, so all ranks return the same final fp32
     latents [n_img, 16, h, w]. Weights are replicated. Latents and embeddings are broadcast from the group's
-    first rank first (ranks may have drawn different noise)."""
+    first rank first (ranks may have drawn different noise). ring=True moves the self-attention's keys as N - 1
+    neighbour shifts (ring attention), each overlapped with the attention over the previous block, instead of
+    one all-gather."""
     import torch.distributed as dist
 
     from .pipeline import flow_schedule
@@ -187,7 +212,8 @@ def sequence_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Te
     nseq, L = ctx.shape[0], ctx.shape[1]
     sched = flow_schedule(num_inference_steps, lh, lw, alpha)
     acc = lat.float().contiguous()
-    eng.set_sequence_parallel(rank, n, lambda s, r: all_gather_rows(s, r, group))
+    eng.set_sequence_parallel(rank, n, lambda s, r: all_gather_rows(s, r, group),
+                              (lambda s, r: ring_shift_rows(s, r, group)) if ring else None)
     try:
         eng.prepare(nseq, lh, lw, nseq * L, num_inference_steps, device=dev)
         eng.set_context(ctx.reshape(nseq * L, -1).contiguous(), [i * L for i in range(nseq + 1)])

@@ -103,6 +103,7 @@ class FLitePipeline:
         self._cfg_group = None
         self._seq_parallel = False
         self._sp_group = None
+        self._sp_ring = False
 
     # ---------------------------------------------------------------- loading
     @classmethod
@@ -176,16 +177,17 @@ class FLitePipeline:
     def disable_cfg_parallel(self):
         self._cfg_parallel = False
 
-    def enable_sequence_parallel(self, group=None):
+    def enable_sequence_parallel(self, group=None, ring: bool = False):
         """Single-image latency over every rank of `group` (no reference counterpart):
         each rank computes a slice of the token rows of every DiT launch, exchanging K/V rows per block
-        (distributed.sequence_parallel_sample). Every rank calls the pipeline with the same inputs and gets the
-        same images."""
+        (distributed.sequence_parallel_sample; ring=True: N - 1 neighbour shifts instead of one all-gather).
+        Every rank calls the pipeline with the same inputs and gets the same images."""
         import torch.distributed as dist
 
         if not (dist.is_available() and dist.is_initialized()):
             raise ValueError("enable_sequence_parallel needs an initialised torch.distributed process group")
         self._sp_group = group
+        self._sp_ring = bool(ring)
         self._seq_parallel = True
 
     def disable_sequence_parallel(self):
@@ -297,7 +299,8 @@ class FLitePipeline:
             from .distributed import sequence_parallel_sample
 
             acc = sequence_parallel_sample(dit, latents, prompt_embeds, negative_prompt_embeds, num_inference_steps,
-                                           guidance_scale, alpha, group=self._sp_group)
+                                           guidance_scale, alpha, group=self._sp_group,
+                                           ring=self._sp_ring)
         elif self._cfg_parallel and do_cfg:
             if apg_config.enabled:
                 raise NotImplementedError("APG is not available in the CFG-parallel mode")

@@ -267,6 +267,14 @@ typedef int (*flite_sp_allgather_fn)(void* user, int which, void* stream);
 int flite_dit_set_sequence_parallel(flite_dit* dit, int rank, int nranks, flite_sp_allgather_fn fn, void* user);
 int flite_dit_sp_buffer_bytes(flite_dit* dit, long* kv_send_bytes, long* out_send_bytes);
 int flite_dit_sp_bind_buffers(flite_dit* dit, void* kv_send, void* kv_recv, void* out_send, void* out_recv);
+/* Ring exchange for the self-attention's keys (ring != 0; default 0 = one all-gather overlapped with the own-key
+ * attention). The K/V rows then travel as N - 1 neighbour shifts, each overlapped with the attention over the
+ * previous block: `fn(user, which >= 2, stream)` is shift k = which - 1 (k = 1 .. N-1) and must send a block of
+ * kv_send bytes to rank (r + 1) mod N and receive one from rank (r - 1) mod N, on `stream`. Source: kv_send for
+ * k = 1, else kv_recv slot (k - 2) & 1; destination: kv_recv slot (k - 1) & 1 (slot i = bytes
+ * [i * kv_send_bytes, (i + 1) * kv_send_bytes) of kv_recv). RCCL send/recv over one xGMI link; gloo in tests.
+ * Falls back to the all-gather when some rank holds no key ((N - 1) * Tl >= T). */
+int flite_dit_sp_set_ring(flite_dit* dit, int ring);
 
 /*
  * 3x3 convolution, padding 1, stride 1 (nn.Conv2d of the diffusers VAE decoder), optionally preceded by a

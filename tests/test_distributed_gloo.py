@@ -44,6 +44,41 @@ def _rows_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _ring_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from f_lite.distributed import ring_shift_rows
+
+    # the engine's buffer protocol (flite.h, flite_dit_sp_set_ring): shift k sends kv_send (k = 1) or ring slot
+    # (k - 2) & 1 and receives into slot (k - 1) & 1; the attention of step k reads slot (k - 1) & 1
+    send = torch.full((6,), rank + 1, dtype=torch.uint8)
+    slots = torch.zeros(2 * 6, dtype=torch.uint8)
+    slot = lambda i: slots[6 * i:6 * (i + 1)]  # noqa: E731
+    seen = []
+    for k in range(1, world):
+        ring_shift_rows(send if k == 1 else slot((k - 2) & 1), slot((k - 1) & 1))
+        seen.append(int(slot((k - 1) & 1)[0]) - 1)
+    q.put((rank, seen))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ring_shift_rows(world):
+    """The ring exchange of the sequence-parallel mode (distributed.ring_shift_rows): after shift k every rank
+    holds the block of rank (r - k) mod N, so the N - 1 steps visit every other rank's keys exactly once."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ring_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=60) for _ in range(world))
+    for p in procs:
+        p.join(30)
+    for r in range(world):
+        assert res[r] == [(r - k) % world for k in range(1, world)]
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_all_gather_rows(world):
     """The sequence-parallel exchange (distributed.all_gather_rows): rank-ordered concatenation."""

@@ -9,8 +9,9 @@ the last rank (T = 80 and 1040 are not multiples of 3). The 512^2 case runs the 
 so the gathered keys take the attention kernel's multi-tile and tail-split paths.
 
 By default the K/V exchange overlaps the attention over each rank's own keys (a partial (O, l) launch, then
-one over the other ranks' keys that adds it: dit.cpp sp_self_attention); `overlap=False` runs the gather-first
-path (FLITE_SP_NO_OVERLAP=1), one attention over every key.
+one over the other ranks' keys that adds it: dit.cpp sp_self_attention); `gather` runs the gather-first
+path (FLITE_SP_NO_OVERLAP=1), one attention over every key; `ring` moves the keys as N - 1 neighbour shifts
+(dit.cpp sp_ring_attention: part_mode 1, then 3 per intermediate block, then 2), the ring-attention schedule.
 """
 import os
 import socket
@@ -55,9 +56,9 @@ def _inputs(case):
     return lat, pos, neg
 
 
-def _worker(rank, world, port, case, q, overlap=True):
+def _worker(rank, world, port, case, q, mode="overlap"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    if not overlap:
+    if mode == "gather":
         os.environ["FLITE_SP_NO_OVERLAP"] = "1"
     try:
         torch.cuda.set_device(0)
@@ -67,11 +68,11 @@ def _worker(rank, world, port, case, q, overlap=True):
         lat, pos, neg = _inputs(case)
         m = DiT.random(seed=0, device="cuda", **CASES[case]["preset"])
         acc = sequence_parallel_sample(m, lat.cuda(), pos.cuda(), neg.cuda(), num_inference_steps=STEPS,
-                                       guidance_scale=G)
+                                       guidance_scale=G, ring=mode == "ring")
         out = [acc.cpu()]
         if case == "tiny":  # the pipeline surface, and the engine back on whole sequences afterwards
             pipe = FLitePipeline(m)
-            pipe.enable_sequence_parallel()
+            pipe.enable_sequence_parallel(ring=mode == "ring")
             h, w = 8 * lat.shape[-2], 8 * lat.shape[-1]
             out.append(pipe(prompt_embeds=pos.cuda(), negative_prompt_embeds=neg.cuda(), latents=lat.cuda(),
                             height=h, width=w, num_inference_steps=STEPS, guidance_scale=G,
@@ -89,11 +90,11 @@ def _worker(rank, world, port, case, q, overlap=True):
         q.put((rank, repr(e)))
 
 
-def _run(case, world, overlap=True):
+def _run(case, world, mode="overlap"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, overlap)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -119,17 +120,18 @@ def _batched(case):
                             use_graph=False).images.float().cpu()
 
 
-@pytest.mark.parametrize("case,world,overlap", [("tiny", 2, True), ("tiny", 3, True), ("10b_d2_512", 2, True),
-                                                ("10b_d2_512", 3, True), ("tiny", 3, False),
-                                                ("10b_d2_512", 3, False)])
-def test_sequence_parallel_matches_whole_sequence_loop(case, world, overlap):
-    res = _run(case, world, overlap)
+@pytest.mark.parametrize("case,world,mode", [("tiny", 2, "overlap"), ("tiny", 3, "overlap"),
+                                             ("10b_d2_512", 2, "overlap"), ("10b_d2_512", 3, "overlap"),
+                                             ("tiny", 3, "gather"), ("10b_d2_512", 3, "gather"),
+                                             ("tiny", 2, "ring"), ("tiny", 4, "ring"), ("10b_d2_512", 3, "ring")])
+def test_sequence_parallel_matches_whole_sequence_loop(case, world, mode):
+    res = _run(case, world, mode)
     got = res[0][0]
     for r in range(1, world):
         assert torch.equal(res[r][0], got), f"rank {r} differs from rank 0"
     batched = _batched(case)
     p_b = R.psnr(got, batched)
-    msg = f"sequence-parallel x{world} ({case}, {'overlapped' if overlap else 'gather-first'}): {p_b:.2f} dB " \
+    msg = f"sequence-parallel x{world} ({case}, {mode}): {p_b:.2f} dB " \
           "vs the whole-sequence loop"
     lat, pos, neg = _inputs(case)
     import dataclasses
