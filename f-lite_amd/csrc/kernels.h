@@ -80,7 +80,8 @@ struct AttnParams {
   // Partial (O, l) hand-over between two launches over disjoint key sets of the same queries (bounded softmax
   // only: with the fixed shift the two partial sums add without rescaling; the sequence-parallel overlap).
   // 1: write the unnormalised O (fp32, [query row][H * 256]) and the row sums l ([query row][H]) instead of o;
-  // 2: add them to this launch's O and l, then normalise into o. No tail split in either mode.
+  // 2: add them to this launch's O and l, then normalise into o; 3: add them and write the sums back as the new
+  // partial (a middle step of the ring, dit.cpp sp_ring_attention). No tail split in any partial mode.
   int part_mode = 0;
   float* part_o = nullptr;
   float* part_l = nullptr;
