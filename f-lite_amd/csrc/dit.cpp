@@ -24,6 +24,12 @@ bool fuse_qk_norm() {
   return on;
 }
 
+// The norm passes read the next GEMM's weights ahead (NormModParams::pf); FLITE_NO_WPREFETCH=1 turns it off (A/B)
+bool w_prefetch() {
+  static const bool on = getenv("FLITE_NO_WPREFETCH") == nullptr;
+  return on;
+}
+
 bool parse_block(const std::string& name, int* idx, std::string* rest) {
   if (name.rfind("blocks.", 0) != 0) return false;
   const size_t dot = name.find('.', 7);
@@ -474,8 +480,16 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   const float *shift_ca = mod + 3L * D, *scale_ca = mod + 4L * D, *gate_ca = mod + 5L * D;
   const float *shift_mlp = mod + 6L * D, *scale_mlp = mod + 7L * D, *gate_mlp = mod + 8L * D;
 
-  auto norm = [&](const bf16_t* w, const float* sh, const float* sc) -> int {
+  // pf0/pf1: weights of the GEMM that reads this norm's output, read ahead into the Infinity Cache (w_prefetch)
+  auto norm = [&](const bf16_t* w, const float* sh, const float* sc, const bf16_t* pf0 = nullptr, long pf0_n = 0,
+                  const bf16_t* pf1 = nullptr, long pf1_n = 0) -> int {
     NormModParams nm;
+    if (w_prefetch()) {
+      nm.pf[0] = pf0;
+      nm.pf_bytes[0] = pf0_n * 2;
+      nm.pf[1] = pf1;
+      nm.pf_bytes[1] = pf1_n * 2;
+    }
     nm.x = x_;
     nm.ldx = D;
     nm.y = nbuf_;
@@ -576,7 +590,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
 
   // --- cross attention (model.py:291-297) ---
   if (b.cross) {
-    if (norm(b.norm2, shift_ca, scale_ca)) return 1;
+    if (norm(b.norm2, shift_ca, scale_ca, b.cq_w, (long)D * D)) return 1;
     GemmParams g;
     g.A = nbuf_;
     g.lda = D;

@@ -123,6 +123,10 @@ struct NormModParams {
   uint8_t* y8 = nullptr;
   uint8_t* ysc = nullptr;
   long ysc_rows_pad = 0;
+  // optional read-ahead (D = 3072 row kernel): up to two byte ranges the next GEMM reads (its weights), touched
+  // once by the workgroups of this pass so that they come from the Infinity Cache instead of HBM
+  const void* pf[2] = {nullptr, nullptr};
+  long pf_bytes[2] = {0, 0};
 };
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s);
 
