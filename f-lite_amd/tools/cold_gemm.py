@@ -4,7 +4,8 @@ In the sampling loop the proj / cross-q / qkv GEMMs run 11-16 % slower than back
 (profiles/r02al vs r02an). Between two uses of a block's weights the loop streams ~10 GB, so every launch starts
 with its weights (and often its activations) beyond the 256 MiB Infinity Cache. This times single launches after
 a 1 GiB flush write, optionally re-touching one operand (weights W, activations A, the fp32 residual x of the
-gated epilogue) right before, against warm back-to-back launches.
+gated epilogue) right before, or rewriting A (A_written: what a producing kernel leaves), against warm
+back-to-back launches.
 """
 import sys
 from pathlib import Path
@@ -52,7 +53,7 @@ def main(reps=8):
         def touch(t):  # read every byte once (a reduction: no temporary copy of t)
             sink.add_(t.sum().float() * 0)  # noqa: B023
 
-        modes = {"warm": None, "cold": [], "cold+W": wts, "cold+A": [a]}
+        modes = {"warm": None, "cold": [], "cold+W": wts, "cold+A": [a], "cold+A_written": ["write", a]}
         if x is not None:
             modes["cold+x"] = [x]
         line = [name]
@@ -61,8 +62,12 @@ def main(reps=8):
             for _ in range(reps):
                 if pre is not None:
                     flush.fill_(1.0)
-                    for t in pre:
-                        touch(t)
+                    if pre and isinstance(pre[0], str):  # rewrite the operand (as the producing kernel would)
+                        for t in pre[1:]:
+                            t.normal_()
+                    else:
+                        for t in pre:
+                            touch(t)
                 else:
                     run()
                 s = torch.cuda.Event(enable_timing=True)
