@@ -568,10 +568,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
     }
   }
   int m0, n0;
-  if (!CONV && sk::use_band(num_n, gridDim.x))
-    sk::tile_origin_band(blockIdx.x, num_m, num_n, m0, n0, Cta::BMV, BN);
-  else
-    sk::tile_origin(wg, num_m, num_n, m0, n0, Cta::BMV, BN);
+  sk::tile_origin(wg, num_m, num_n, m0, n0, Cta::BMV, BN);
   c.setup_tile(m0, n0);
   c.mainloop(acc, 0, nk);
   c.epilogue(acc, m0, n0);

@@ -487,10 +487,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_fp8_kernel(GemmFp8Params p) {
     }
   }
   int m0, n0;
-  if (sk::use_band(num_n, gridDim.x))
-    sk::tile_origin_band(blockIdx.x, num_m, num_n, m0, n0, Cta::WM * 2, BN);
-  else
-    sk::tile_origin(wg, num_m, num_n, m0, n0, Cta::WM * 2, BN);
+  sk::tile_origin(wg, num_m, num_n, m0, n0, Cta::WM * 2, BN);
   c.setup_tile(m0, n0);
   c.mainloop(acc, 0, nk);
   c.epilogue(acc, m0, n0);

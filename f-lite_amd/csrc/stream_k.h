@@ -26,26 +26,6 @@ __device__ __forceinline__ void tile_origin(int L, int num_m, int num_n, int& m0
   n0 = (rem / gm) * bn;
 }
 
-// Data-parallel launches whose N-tile count splits evenly over the 8 XCDs (the SwiGLU gate/up GEMM: 96): XCD x
-// owns the N-panels [x nb, (x + 1) nb) for every M-tile, swept as N-groups of GN panels by M blocks of GM tiles
-// (block b runs on XCD b % 8 as that XCD's (b >> 3)-th tile). Each weight panel is then first read from HBM by one
-// XCD, its band's panels arrive a group at a time over the whole launch instead of most of the 151 MB in the first
-// rounds, and the activation panels (just written by the previous kernel) are what the XCDs share. In the sampling
-// loop the weights are cold: after a cache flush with A freshly written, gate/up 1021 -> 962 us (profiles/r02aw);
-// warm back to back +0.5-1 %.
-__device__ __forceinline__ bool use_band(int num_n, int grid) { return (num_n & 7) == 0 && (grid & 7) == 0; }
-__device__ __forceinline__ void tile_origin_band(int b, int num_m, int num_n, int& m0, int& n0, int bm, int bn) {
-  const int x = b & 7, j = b >> 3;
-  const int nb = num_n >> 3;
-  const int GN = (nb % 4 == 0) ? 4 : nb, GM = 8;
-  const int per_ng = num_m * GN;
-  const int ng = j / per_ng, r = j - ng * per_ng;
-  const int mb = r / (GM * GN), rr = r - mb * (GM * GN);
-  const int gm = min(GM, num_m - mb * GM);
-  m0 = (mb * GM + rr % gm) * bm;
-  n0 = (x * nb + ng * GN + rr / gm) * bn;
-}
-
 __device__ __forceinline__ long sk_start(int g, long I, int G) { return (long)g * I / G; }
 
 // Stream-K + data-parallel (persistent grid G = one workgroup per CU) over 256x256 tiles. Tiles [0, sk_tiles)
