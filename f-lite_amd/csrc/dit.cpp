@@ -534,6 +534,10 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.bias = b.qkv_b;
     g.out = qkv_;
     g.ldo = 3L * D;
+    if (w_prefetch()) {  // the proj weights, read after the attention, into the Infinity Cache
+      g.pf = b.proj_w;
+      g.pf_bytes = (long)D * D * 2;
+    }
     g.M = (int)M_;
     g.N = 3 * D;
     g.K = D;
@@ -599,6 +603,10 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.bias = b.cq_b;
     g.out = qkv_;
     g.ldo = D;
+    if (w_prefetch()) {  // the cross-proj weights, read after the cross-attention
+      g.pf = b.cproj_w;
+      g.pf_bytes = (long)D * D * 2;
+    }
     g.M = (int)M_;
     g.N = D;
     g.K = D;

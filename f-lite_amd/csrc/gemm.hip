@@ -34,6 +34,9 @@ constexpr int TILE_BYTES = BM * BK * 2;          // 32 KiB per operand tile
 // LDS: [A buf0 | A buf1 | W buf0 | W buf1]: every fragment read is a per-lane base + 16-bit immediate
 constexpr int W_REGION = 2 * TILE_BYTES;
 constexpr int LDS_BYTES = 4 * TILE_BYTES;        // 128 KiB
+// + 8 KiB that nothing reads: the landing area of the weight read-ahead (GemmCta::read_ahead)
+constexpr int PF_LDS = 8192;
+constexpr int LDS_ALLOC = LDS_BYTES + PF_LDS;
 
 typedef __attribute__((ext_vector_type(4))) int i32x4;
 
@@ -219,6 +222,33 @@ struct GemmCta {
     }
     stage_dma(a_rsrc, sa, va[0], va[1], va[2], va[3], w_rsrc, kb, w_off[0], w_off[1], w_off[2], w_off[3], la, lw,
               (unsigned)__builtin_amdgcn_readfirstlane(kt >= ke ? 1 : 0));
+  }
+
+  // Weight read-ahead for the GEMM after next (GemmParams::pf): this workgroup's 8 KiB pieces wg, wg + G, ... of
+  // the range (at most 6), one 1 KiB LDS-DMA copy per wave each, into the PF_LDS area that nothing reads. Issued
+  // after the mainloop, so their HBM latency overlaps the epilogue; the kernel waits for them at its end.
+  __device__ __forceinline__ void read_ahead(int wg, int G) {
+    const long pieces = (p.pf_bytes + 8191) >> 13;
+    if (wg >= pieces) return;
+    const i32x4 rs = make_rsrc(p.pf, (unsigned)p.pf_bytes);
+    const unsigned lds = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds0 + LDS_BYTES + wave * 1024));
+    const unsigned voff = (unsigned)(wave * 1024 + lane * 16);
+#pragma unroll 1
+    for (int k = 0; k < 6; ++k) {
+      const long i = wg + (long)k * G;
+      if (i >= pieces) break;
+      const unsigned soff = (unsigned)__builtin_amdgcn_readfirstlane((int)(i << 13));
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %[keep], m0\n\t"
+          "s_mov_b32 m0, %[l]\n\t"
+          "s_nop 0\n\t"
+          "buffer_load_dwordx4 %[v], %[r], %[s] offen lds\n\t"
+          "s_mov_b32 m0, %[keep]"
+          : [keep] "=&s"(keep)
+          : [l] "s"(lds), [r] "s"(rs), [s] "s"(soff), [v] "v"(voff)
+          : "memory");
+    }
   }
 
   // W fragment ni / A fragment mi of k-step s in buffer BUF
@@ -571,7 +601,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
   sk::tile_origin(wg, num_m, num_n, m0, n0, Cta::BMV, BN);
   c.setup_tile(m0, n0);
   c.mainloop(acc, 0, nk);
+  if constexpr (!CONV)
+    if (p.pf != nullptr) c.read_ahead(wg, gridDim.x);
   c.epilogue(acc, m0, n0);
+  if constexpr (!CONV)
+    if (p.pf != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the read-ahead has landed
 }
 
 int g_num_cu = 0;
@@ -602,14 +636,14 @@ int launch(GemmParams p, hipStream_t s) {
   p.sk_tiles = choose_sk_tiles(p, T, &p.sk_wgs);
   if (p.conv_in != nullptr) {
     if constexpr (EPI == EPI_STORE_BF16 || EPI == EPI_STORE_F32)  // gemm_bf16 admits only these with CONV
-      hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true, 8>), dim3(T), dim3(NT), LDS_BYTES, s, p);
+      hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true, 8>), dim3(T), dim3(NT), LDS_ALLOC, s, p);
   } else if (p.sk_tiles) {
-    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(g_num_cu), dim3(NT), LDS_BYTES, s, p);
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(g_num_cu), dim3(NT), LDS_ALLOC, s, p);
   } else if (use_bm224(p)) {
     const int T224 = (p.M + 223) / 224 * num_n;
-    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 7>), dim3(T224), dim3(NT), LDS_BYTES, s, p);
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 7>), dim3(T224), dim3(NT), LDS_ALLOC, s, p);
   } else {
-    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(T), dim3(NT), LDS_BYTES, s, p);
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(T), dim3(NT), LDS_ALLOC, s, p);
   }
   return 0;
 }
@@ -619,14 +653,14 @@ bool attrs_done = false;
 template <int EPI>
 hipError_t set_attrs() {
   hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, false, 8>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, false, 7>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          LDS_BYTES);
+                          LDS_ALLOC);
   if (e != hipSuccess) return e;
   if constexpr (EPI == EPI_STORE_BF16 || EPI == EPI_STORE_F32)
     return hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, true, 8>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC);
   return hipSuccess;
 }
 
@@ -648,7 +682,7 @@ int gemm_init() {
     g_num_cu = prop.multiProcessorCount;
     int per_cu = 0;  // the stream-K grid needs every workgroup resident at once
     FLITE_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gemm_bf16_kernel<EPI_RESID_F32, false, 8>, NT,
-                                                                LDS_BYTES));
+                                                                LDS_ALLOC));
     if (per_cu < 1) g_num_cu = 0;
   }
   attrs_done = true;
@@ -671,6 +705,7 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
   FLITE_REQUIRE(p.ldw % 8 == 0, "gemm: ldw must be a multiple of 8 elements");
   FLITE_REQUIRE(((uintptr_t)p.W & 15) == 0, "gemm: W must be 16-B aligned");
   FLITE_REQUIRE((long)p.N * p.ldw * 2 < (1L << 32), "gemm: W must be < 4 GiB (32-bit buffer offsets)");
+  FLITE_REQUIRE(p.pf == nullptr || (p.pf_bytes > 0 && p.pf_bytes < (1L << 31)), "gemm: read-ahead range must be < 2 GiB");
   if (p.conv_in != nullptr) {
     FLITE_REQUIRE(p.conv_c % 64 == 0, "conv: input channels must be a multiple of 64");
     FLITE_REQUIRE(p.K == 9 * p.conv_c, "conv: K must be 9 * C_in");

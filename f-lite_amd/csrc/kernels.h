@@ -46,6 +46,10 @@ struct GemmParams {
   RopeAxes rope;
   int rope_cols = 0, norm_cols = 0;
   float norm_eps = 1e-6f;
+  // optional read-ahead (data-parallel tiles): a byte range a later kernel reads (its weights), touched by the
+  // workgroups after their mainloops so that it comes from the Infinity Cache instead of HBM
+  const void* pf = nullptr;
+  long pf_bytes = 0;
 };
 
 // bytes of the stream-K workspace (partials + flags) for the current device
