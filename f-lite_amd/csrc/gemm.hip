@@ -705,7 +705,8 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
   FLITE_REQUIRE(p.ldw % 8 == 0, "gemm: ldw must be a multiple of 8 elements");
   FLITE_REQUIRE(((uintptr_t)p.W & 15) == 0, "gemm: W must be 16-B aligned");
   FLITE_REQUIRE((long)p.N * p.ldw * 2 < (1L << 32), "gemm: W must be < 4 GiB (32-bit buffer offsets)");
-  FLITE_REQUIRE(p.pf == nullptr || (p.pf_bytes > 0 && p.pf_bytes < (1L << 31)), "gemm: read-ahead range must be < 2 GiB");
+  FLITE_REQUIRE(p.pf == nullptr || (p.pf_bytes > 0 && p.pf_bytes < (1L << 31)),
+                "gemm: read-ahead range must be < 2 GiB");
   if (p.conv_in != nullptr) {
     FLITE_REQUIRE(p.conv_c % 64 == 0, "conv: input channels must be a multiple of 64");
     FLITE_REQUIRE(p.K == 9 * p.conv_c, "conv: K must be 9 * C_in");
