@@ -19,7 +19,6 @@ SHAPES = [  # name, M, N, K, epilogue
     ("cross_q", 8224, 3072, 3072, "store"),
     ("qkv", 8224, 9216, 3072, "store"),
     ("gateup", 8224, 24576, 3072, "swiglu"),
-    ("down", 8224, 3072, 12288, "resid"),
 ]
 
 
@@ -53,7 +52,8 @@ def main(reps=8):
         def touch(t):  # read every byte once (a reduction: no temporary copy of t)
             sink.add_(t.sum().float() * 0)  # noqa: B023
 
-        modes = {"warm": None, "cold": [], "cold+W": wts, "cold+A": [a], "cold+A_written": ["write", a]}
+        modes = {"warm": None, "cold": [], "cold+W": wts, "cold+A": [a], "cold+A_written": ["write", a],
+                 "cold+A_written+read": ["write+read", a]}
         if x is not None:
             modes["cold+x"] = [x]
         line = [name]
@@ -65,6 +65,8 @@ def main(reps=8):
                     if pre and isinstance(pre[0], str):  # rewrite the operand (as the producing kernel would)
                         for t in pre[1:]:
                             t.normal_()
+                            if pre[0] == "write+read":  # and read it back in another kernel
+                                touch(t)
                     else:
                         for t in pre:
                             touch(t)
