@@ -169,6 +169,49 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
     }
 
 
+def cpu_baseline_full(model, vae, cfg: dict, H: int, W: int, steps: int, k_steps: int = 2):
+    """BASELINE.md §4's plan: K whole CFG-batched denoise steps of the fp32 CPU port (every block, the CFG
+    combine and Euler update) + one VAE decode, per image = (steps / K) x the K steps + the decode, labelled
+    extrapolated. Minutes of CPU at 10B 1024^2: a one-off measurement (`--cpu-baseline-full K`), not part of
+    the default bounded bench."""
+    from oracle import flite_ref as R
+    from oracle import vae_ref as VR
+
+    threads = cpu_threads()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    rcfg = R.DiTConfig(**{k: cfg[k] for k in ("in_channels", "patch_size", "hidden_size", "depth", "num_heads",
+                                                 "mlp_ratio", "cross_attn_input_size", "train_bias_and_rms",
+                                                 "per_block_adaln")})
+    params = {n: t.detach().float().cpu() for n, t in model.named_parameters()}
+    ref = R.RefDiT(rcfg, params, dtype=torch.float32)
+    g = torch.Generator().manual_seed(0)
+    lat = torch.randn(1, cfg["in_channels"], H // 8, W // 8, generator=g)
+    pos = torch.randn(1, 512, cfg["cross_attn_input_size"], generator=g)
+    res = {}
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        R.sample(ref, lat, pos, torch.zeros_like(pos), num_steps=steps, guidance_scale=6.0, height=H, width=W,
+                 t_dtype=torch.bfloat16, acc_dtype=torch.float32, max_steps=k_steps)
+        res["dit_steps_s"] = time.perf_counter() - t0
+        res["vae_s"] = 0.0
+        if vae is not None:
+            dec = VR.RefVAEDecoder({n: t.detach().float().cpu() for n, t in vae.named_parameters()})
+            t0 = time.perf_counter()
+            VR.decode_to_uint8(dec, lat)
+            res["vae_s"] = time.perf_counter() - t0
+    torch.set_num_threads(prev_threads)
+    per_image = res["dit_steps_s"] * steps / k_steps + res["vae_s"]
+    return {
+        "value": 1.0 / per_image, "unit": "images/s", "cores": threads, "kind": "port", "extrapolated": True,
+        "sample": (f"fp32 CPU port (oracle/flite_ref.py sample loop + oracle/vae_ref.py) at {H}x{W}: {k_steps} whole "
+                   f"CFG-6 steps of the {steps}-step schedule {res['dit_steps_s']:.1f} s, VAE decode "
+                   f"{res['vae_s']:.1f} s; per image = {steps}/{k_steps} x {res['dit_steps_s']:.1f} + "
+                   f"{res['vae_s']:.1f} = {per_image:.0f} s (EXTRAPOLATED x{steps / k_steps:g}, BASELINE.md §4)"),
+        "host": host_info(), "components_s": {k: round(v, 3) for k, v in res.items()},
+    }
+
+
 def relaunch_distributed(n: int) -> int:
     """`bench.py --gpus N` run without torchrun: start the N ranks as a child torch.distributed.run (one process
     per GPU, 127.0.0.1 rendezvous) and return its exit code. Called before anything touches the GPU."""
@@ -199,6 +242,9 @@ def main():
     ap.add_argument("--vae-tiling", action="store_true",
                     help="pipe.enable_vae_tiling() as generate.py:77-78 does (tiled decode above 1024 px)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-full", type=int, default=0, metavar="K",
+                    help="CPU baseline from K whole CFG steps + VAE (BASELINE.md §4; minutes of CPU) instead of the "
+                         "bounded per-component sample")
     ap.add_argument("--images-per-gpu", type=int, default=1,
                     help="images per bench step and GPU, sampled as ONE batch (num_images_per_prompt; M = 2 x B x T)")
     ap.add_argument("--fp8", action="store_true",
@@ -347,7 +393,11 @@ def main():
                 pass
     cpu = None
     if not args.no_cpu_baseline:  # rank 0 only (the other ranks have returned), at every N
-        cpu = cpu_baseline_sample(model, vae, cfg, args.height, args.width, args.sample_steps)
+        if args.cpu_baseline_full > 0:
+            cpu = cpu_baseline_full(model, vae, cfg, args.height, args.width, args.sample_steps,
+                                    args.cpu_baseline_full)
+        else:
+            cpu = cpu_baseline_sample(model, vae, cfg, args.height, args.width, args.sample_steps)
 
     metric = "images/sec @%dx%d, %d steps, F-Lite-%s %s" % (args.width, args.height, args.sample_steps,
                                                             args.model.upper(), "fp8" if args.fp8 else "bf16")

@@ -69,7 +69,8 @@ def build(force: bool = False, verbose: bool = True) -> Path:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     newest = max(o.stat().st_mtime for o in objs)
     if force or not LIB.exists() or LIB.stat().st_mtime < newest:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs),
+               "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

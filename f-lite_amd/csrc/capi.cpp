@@ -287,6 +287,19 @@ int flite_cfg_euler(void* stream, const float* uncond, const float* cond, float*
   return cfg_euler_nchw(uncond, cond, acc, n, guidance, dt, use_cfg, (hipStream_t)stream);
 }
 
+int flite_apg_sums(void* stream, const float* uncond, const float* cond, long n, float k, int phase, float* out2) {
+  FLITE_REQUIRE(uncond && cond && out2, "flite_apg_sums: null argument");
+  FLITE_REQUIRE(n >= 0, "flite_apg_sums: negative element count");
+  return apg_sums(uncond, cond, n, k, phase, out2, (hipStream_t)stream);
+}
+
+int flite_apg_euler(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
+                    float k, float orth_scale, float dt) {
+  FLITE_REQUIRE(uncond && cond && acc, "flite_apg_euler: null argument");
+  FLITE_REQUIRE(n >= 0, "flite_apg_euler: negative element count");
+  return apg_update_nchw(uncond, cond, acc, n, guidance, k, orth_scale, dt, (hipStream_t)stream);
+}
+
 int flite_dit_forward(flite_dit* dit, void* stream, const void* x, int x_is_bf16, int batch, int t_row0,
                       int t_row_step, void* out, int out_is_bf16) {
   FLITE_REQUIRE(dit && x && out, "flite_dit_forward: null argument");
@@ -451,5 +464,10 @@ int flite_rmsnorm_modulate_fp8(void* stream, const float* x, long ldx, void* y8,
 int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable) {
   FLITE_REQUIRE(dit, "flite_dit_enable_fp8: null engine");
   return dit->eng->enable_fp8((hipStream_t)stream, enable != 0);
+}
+
+int flite_dit_weights_updated(flite_dit* dit, void* stream) {
+  FLITE_REQUIRE(dit, "flite_dit_weights_updated: null engine");
+  return dit->eng->weights_updated((hipStream_t)stream);
 }
 }  // extern "C"

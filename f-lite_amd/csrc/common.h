@@ -163,3 +163,15 @@ const char* get_last_error();
       return 2;                                                                       \
     }                                                                                 \
   } while (0)
+
+// roctx ranges (rocprofv3 --marker-trace): host-side markers per denoise step / DiT block / VAE decode, so kernel
+// traces split by phase. Near-free without a tool attached; inside a hipGraph capture they mark the capture.
+#include <rocprofiler-sdk-roctx/roctx.h>
+namespace flite {
+struct RoctxRange {
+  explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+  ~RoctxRange() { roctxRangePop(); }
+  RoctxRange(const RoctxRange&) = delete;
+  RoctxRange& operator=(const RoctxRange&) = delete;
+};
+}  // namespace flite

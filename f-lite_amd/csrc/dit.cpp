@@ -134,10 +134,9 @@ int DitEngine::bind(const std::string& name, const void* ptr, long numel) {
   auto old = bound_.find(name);
   if (old == bound_.end() || old->second.first != ptr) {
     drop_graph();
-    if (!w8_.empty()) {  // the fp8 copies were quantised from the old storage
-      free_fp8_weights();
-      fp8_ = false;
-    }
+    // the fp8 copies were quantised from the old storage: fp8 mode stays on and the next forward / sample
+    // requantises them (into the same buffers) before it runs
+    w8_stale_ = true;
   }
   bound_[name] = {ptr, numel};
   const bf16_t* p = (const bf16_t*)ptr;
@@ -699,36 +698,53 @@ int DitEngine::enable_fp8(hipStream_t s, bool on) {
   }
   if (check_bound()) return 2;
   FLITE_REQUIRE(D % 128 == 0 && F % 128 == 0, "fp8: hidden and MLP widths must be multiples of 128");
-  if (w8_.empty()) {
-    w8_.resize(cfg.depth);
-    auto buf = [&](uint8_t** p, size_t bytes) -> int {
-      FLITE_HIP_CHECK(hipMalloc((void**)p, bytes));
-      w8_allocs_.push_back(*p);
-      return 0;
-    };
-    // weight [rows, K] -> fp8 + scales [K/128][rows][4] (rows are multiples of 256 for every DiT weight)
-    auto q = [&](const bf16_t* w, long rows, int K, uint8_t** d, uint8_t** sc) -> int {
-      FLITE_REQUIRE(rows % 256 == 0, "fp8: weight rows must be a multiple of 256");
-      if (buf(d, (size_t)rows * K) || buf(sc, (size_t)(K / 128) * rows * 4)) return 1;
-      return quant_rows_fp8(w, K, rows, K, *d, K, *sc, rows, s);
-    };
-    // fused RoPE epilogue: the q/k rows of the qkv weight in rope_perm order (gemm_fp8 EPI8_QKV_NORM_BF16)
-    const long perm_rows = (fuse_qk_norm() && cfg.use_rope) ? 2L * D : 0;
-    for (int i = 0; i < cfg.depth; ++i) {
-      const BlockW& b = w_.blocks[i];
-      Fp8W& f = w8_[i];
-      if (buf(&f.qkv, (size_t)3 * D * D) || buf(&f.qkv_s, (size_t)(D / 128) * 3 * D * 4) ||
-          quant_rows_fp8_perm(b.qkv_w, D, 3L * D, D, f.qkv, D, f.qkv_s, 3L * D, perm_rows, s))
-        return 1;
-      if (q(b.proj_w, D, D, &f.proj, &f.proj_s) || q(b.down_w, D, F, &f.down, &f.down_s)) return 1;
-      if (b.cross && (q(b.cq_w, D, D, &f.cq, &f.cq_s) || q(b.cproj_w, D, D, &f.cproj, &f.cproj_s))) return 1;
-      if (buf(&f.gu, (size_t)2 * F * D) || buf(&f.gu_s, (size_t)(D / 128) * 2 * F * 4)) return 1;
-      if (quant_gateup_fp8(b.gate_w, b.up_w, D, F, D, f.gu, f.gu_s, s)) return 1;
-    }
-    FLITE_HIP_CHECK(hipStreamSynchronize(s));
-  }
+  // always from the current bf16 weights: they may have changed while fp8 mode was off
+  w8_stale_ = true;
+  if (quantise_fp8(s)) return 1;
   fp8_ = true;
   return alloc_fp8_act();
+}
+
+int DitEngine::weights_updated(hipStream_t s) {
+  w8_stale_ = true;
+  return fp8_ ? quantise_fp8(s) : 0;
+}
+
+// (Re)quantise every block GEMM weight into the engine's MXFP8 copies (allocated once; the sizes depend only on
+// the config). Never called inside a graph capture: forward / sample call it before they launch anything.
+int DitEngine::quantise_fp8(hipStream_t s) {
+  if (!w8_stale_) return 0;
+  if (check_bound()) return 2;
+  const bool fresh = w8_.empty();
+  if (fresh) w8_.resize(cfg.depth);
+  auto buf = [&](uint8_t** p, size_t bytes) -> int {
+    if (!fresh) return 0;
+    FLITE_HIP_CHECK(hipMalloc((void**)p, bytes));
+    w8_allocs_.push_back(*p);
+    return 0;
+  };
+  // weight [rows, K] -> fp8 + scales [K/128][rows][4] (rows are multiples of 256 for every DiT weight)
+  auto q = [&](const bf16_t* w, long rows, int K, uint8_t** d, uint8_t** sc) -> int {
+    FLITE_REQUIRE(rows % 256 == 0, "fp8: weight rows must be a multiple of 256");
+    if (buf(d, (size_t)rows * K) || buf(sc, (size_t)(K / 128) * rows * 4)) return 1;
+    return quant_rows_fp8(w, K, rows, K, *d, K, *sc, rows, s);
+  };
+  // fused RoPE epilogue: the q/k rows of the qkv weight in rope_perm order (gemm_fp8 EPI8_QKV_NORM_BF16)
+  const long perm_rows = (fuse_qk_norm() && cfg.use_rope) ? 2L * D : 0;
+  for (int i = 0; i < cfg.depth; ++i) {
+    const BlockW& b = w_.blocks[i];
+    Fp8W& f = w8_[i];
+    if (buf(&f.qkv, (size_t)3 * D * D) || buf(&f.qkv_s, (size_t)(D / 128) * 3 * D * 4) ||
+        quant_rows_fp8_perm(b.qkv_w, D, 3L * D, D, f.qkv, D, f.qkv_s, 3L * D, perm_rows, s))
+      return 1;
+    if (q(b.proj_w, D, D, &f.proj, &f.proj_s) || q(b.down_w, D, F, &f.down, &f.down_s)) return 1;
+    if (b.cross && (q(b.cq_w, D, D, &f.cq, &f.cq_s) || q(b.cproj_w, D, D, &f.cproj, &f.cproj_s))) return 1;
+    if (buf(&f.gu, (size_t)2 * F * D) || buf(&f.gu_s, (size_t)(D / 128) * 2 * F * 4)) return 1;
+    if (quant_gateup_fp8(b.gate_w, b.up_w, D, F, D, f.gu, f.gu_s, s)) return 1;
+  }
+  FLITE_HIP_CHECK(hipStreamSynchronize(s));
+  w8_stale_ = false;
+  return 0;
 }
 
 // One DiTBlock in fp8 (flite_dit_enable_fp8): the six block GEMMs on MXFP8 operands; attention, RoPE / QK-norm,
@@ -915,6 +931,7 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
   FLITE_REQUIRE(t_row0 >= 0 && t_row0 + (B_ - 1) * t_row_step < nt_, "forward: timestep rows out of range");
   FLITE_REQUIRE(sp_n_ == 1 || (sp_kv_send_ && sp_kv_recv_ && sp_out_send_ && sp_out_recv_),
                 "forward: sequence parallelism needs its exchange buffers (flite_dit_sp_bind_buffers)");
+  if (fp8_ && w8_stale_ && quantise_fp8(s)) return 1;  // a weight was rebound since the fp8 copies were made
   const int cpp = C * P * P;
   // patch embed (model.py:533) straight into the residual stream after the registers (model.py:535)
   if (patchify(lat, lat_bf16, patches_, Bi, C, Hl_, Wl_, P, dup, s)) return 1;
@@ -963,6 +980,9 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
   const long mseg = (long)t_row_step * mod_t_stride_;
   for (int i = 0; i < cfg.depth; ++i) {
     const float* mod = mod_ + (long)t_row0 * mod_t_stride_ + (cfg.per_block_adaln ? (long)i * 9 * D : 0);
+    char name[32];
+    snprintf(name, sizeof(name), "flite.block.%d", i);
+    RoctxRange range(name);
     if (fp8_ ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg)) return 1;
   }
   // final stage (model.py:575-581): drop registers, RMSNorm (fp32 weight multiply), modulate, project
@@ -1173,6 +1193,7 @@ int DitEngine::sp_bind_buffers(void* kv_send, void* kv_recv, void* out_send, voi
 }
 
 int DitEngine::unpatchify_out(hipStream_t s, void* y, bool out_bf16) {
+  FLITE_REQUIRE(fout_ != nullptr && y != nullptr, "unpatchify: call prepare first (and pass an output)");
   return unpatchify(fout_, y, out_bf16, B_, C, Hl_, Wl_, P, s);
 }
 
@@ -1182,6 +1203,7 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
   const int dup = use_cfg ? 2 : 1;
   FLITE_REQUIRE(Bi * dup == B_, "sample: batch does not match the prepared workspace");
   FLITE_REQUIRE(!apg || use_cfg, "sample: APG requires classifier-free guidance");
+  if (fp8_ && w8_stale_ && quantise_fp8(s)) return 1;  // before any capture: quantise_fp8 synchronises
   // timesteps: one row per step, shared by every sample of the batch (pipeline.py:260,268)
   FLITE_HIP_CHECK(hipMemcpyAsync(tdev_, t_host, n_steps * 4, hipMemcpyHostToDevice, s));
   if (set_timesteps(s, tdev_, n_steps, cfg.bf16_timestep_quant)) return 1;
@@ -1189,6 +1211,9 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
   auto body = [&](hipStream_t st, float* acc) -> int {
     probe_n_ = 0;
     for (int i = 0; i < n_steps; ++i) {
+      char name[32];
+      snprintf(name, sizeof(name), "flite.step.%d", i);
+      RoctxRange range(name);
       if (probe_begin(st, FLITE_PROBE_STEP)) return 1;
       if (forward(st, acc, false, Bi, dup, i, 0)) return 1;
       if (probe_end(st, FLITE_PROBE_STEP)) return 1;

@@ -50,6 +50,8 @@ class DitEngine {
 
   // fp8 mode (flite_dit_enable_fp8): MXFP8 copies of the block GEMM weights + fp8 activations
   int enable_fp8(hipStream_t s, bool on);
+  // the bound weights' CONTENTS changed in place (flite_dit_weights_updated): requantise the fp8 copies
+  int weights_updated(hipStream_t s);
 
   // sequence parallelism (flite_dit_set_sequence_parallel)
   int set_sequence_parallel(int rank, int nranks, flite_sp_allgather_fn fn, void* user);
@@ -79,6 +81,7 @@ class DitEngine {
   int sp_gather_out(hipStream_t s);
   int run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg);
   int alloc_fp8_act();
+  int quantise_fp8(hipStream_t s);
   void free_fp8_weights();
   int alloc(void** p, size_t bytes);
   void free_ws();
@@ -142,6 +145,7 @@ class DitEngine {
     uint8_t *cproj = nullptr, *cproj_s = nullptr, *gu = nullptr, *gu_s = nullptr, *down = nullptr, *down_s = nullptr;
   };
   bool fp8_ = false;
+  bool w8_stale_ = true;  // the fp8 copies do not reflect the bound bf16 weights (requantised before the next use)
   std::vector<Fp8W> w8_;
   std::vector<void*> w8_allocs_;
   uint8_t *nbuf8_ = nullptr, *nbuf8_s_ = nullptr, *obuf8_ = nullptr, *obuf8_s_ = nullptr;

@@ -155,6 +155,9 @@ int cfg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, 
 int cfg_euler_nchw(const float* u, const float* c, float* acc, long n, float g, float dt, int use_cfg,
                    hipStream_t s);
 int unpatchify(const float* out, void* y, bool out_bf16, int B, int C, int H, int W, int P, hipStream_t s);
+int apg_sums(const float* u, const float* c, long n, float k, int phase, float* out2, hipStream_t s);
+int apg_update_nchw(const float* u, const float* c, float* acc, long n, float g, float k, float sc, float dt,
+                    hipStream_t s);
 int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, float g, float thr, float dt,
               hipStream_t s);
 int timestep_embed(const float* t, bf16_t* emb, int n, int D, int quantize, hipStream_t s);

@@ -33,6 +33,14 @@ class VaeEngine {
   }
   bool fp8_weights() const { return fp8_w_; }
 
+  // the bound weights changed in place: re-pack (and requantise) now, for the prepared shape
+  int weights_updated() {
+    if (h_ == 0) return 0;  // nothing packed yet: the first prepare packs
+    const int h = h_, w = w_;
+    packed_.clear();
+    return prepare(h, w);
+  }
+
   int bind(const std::string& name, const void* p, long n) {
     FLITE_REQUIRE(p != nullptr && ((uintptr_t)p & 15) == 0, "vae bind: null or unaligned " + name);
     params_[name] = {(const bf16_t*)p, n};
@@ -77,6 +85,7 @@ class VaeEngine {
   // decode one image: z fp32 [C, h, w] -> img uint8 [H, W, 3]
   int decode(hipStream_t s, const float* z, unsigned char* img, float scaling, float shift) {
     FLITE_REQUIRE(h_ > 0, "vae decode: call prepare first");
+    RoctxRange range("flite.vae.decode");
     if (decode_core(s, z, (long)h_ * w_, w_, h_, w_, out32_, scaling, shift)) return 1;
     const long H = (long)h_ << (cfg.n_blocks - 1), W = (long)w_ << (cfg.n_blocks - 1);
     return to_uint8(out32_, 4, img, H * W, s);
@@ -486,6 +495,11 @@ int flite_vae_bind(flite_vae* v, const char* name, const void* ptr, long numel) 
 int flite_vae_enable_fp8_weights(flite_vae* v, int on) {
   FLITE_REQUIRE(v, "flite_vae_enable_fp8_weights: null engine");
   return v->eng->enable_fp8_weights(on != 0);
+}
+
+int flite_vae_weights_updated(flite_vae* v) {
+  FLITE_REQUIRE(v, "flite_vae_weights_updated: null engine");
+  return v->eng->weights_updated();
 }
 
 int flite_vae_prepare(flite_vae* v, int latent_h, int latent_w) {

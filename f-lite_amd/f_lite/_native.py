@@ -78,6 +78,8 @@ SIGNATURES = {
     "flite_dit_forward": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _i]),
     "flite_dit_sample": (_i, [_vp, _vp, _vp, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _f, _i, _i, _f, _i]),
     "flite_cfg_euler": (_i, [_vp, _vp, _vp, _vp, _l, _f, _f, _i]),
+    "flite_apg_sums": (_i, [_vp, _vp, _vp, _l, _f, _i, _vp]),
+    "flite_apg_euler": (_i, [_vp, _vp, _vp, _vp, _l, _f, _f, _f, _f]),
     "flite_conv3x3_pack_weight":(_i, [_vp, _vp, _vp, _i, _i, _i]),
     "flite_conv3x3_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i]),
     "flite_group_norm": (_i, [_vp, _vp, _vp, _l, _i, _i, _vp, _vp, _f, _i, _vp]),
@@ -97,6 +99,8 @@ SIGNATURES = {
                                _l, _i, _vp]),
     "flite_rmsnorm_modulate_fp8": (_i, [_vp, _vp, _l, _vp, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_dit_enable_fp8": (_i, [_vp, _vp, _i]),
+    "flite_dit_weights_updated": (_i, [_vp, _vp]),
+    "flite_vae_weights_updated": (_i, [_vp]),
     "flite_dit_set_sequence_parallel": (_i, [_vp, _i, _i, _vp, _vp]),
     "flite_dit_sp_buffer_bytes": (_i, [_vp, ctypes.POINTER(_l), ctypes.POINTER(_l)]),
     "flite_dit_sp_bind_buffers": (_i, [_vp, _vp, _vp, _vp, _vp]),
@@ -315,6 +319,31 @@ def cfg_euler_(acc, uncond, cond, guidance, dt, use_cfg=True):
     return acc
 
 
+def apg_sums(uncond, cond, k=0.0, phase=0, out=None):
+    """APG's batch-global reductions on fp32 NCHW branch outputs (include/flite.h flite_apg_sums): phase 0 ->
+    [sum c (c - u), sum c^2], phase 1 -> [sum o, sum o^2] with o = (c - u) - k c. A 2-float device tensor."""
+    require_gpu(uncond, "uncond", torch.float32)
+    require_gpu(cond, "cond", torch.float32)
+    if uncond.shape != cond.shape:
+        raise FliteError(f"apg_sums: uncond {tuple(uncond.shape)} and cond {tuple(cond.shape)} differ")
+    out = torch.empty(2, device=cond.device, dtype=torch.float32) if out is None else out
+    check(load().flite_apg_sums(stream_ptr(cond.device), uncond.data_ptr(), cond.data_ptr(), cond.numel(), float(k),
+                                int(phase), out.data_ptr()), "flite_apg_sums")
+    return out
+
+
+def apg_euler_(acc, uncond, cond, guidance, k, orth_scale, dt):
+    """acc += dt * (c + (g - 1) * orth_scale * ((c - u) - k c)) in place (pipeline.py:285-286,296)."""
+    for t, n in ((acc, "acc"), (uncond, "uncond"), (cond, "cond")):
+        require_gpu(t, n, torch.float32)
+        if t.shape != acc.shape:
+            raise FliteError(f"apg_euler: {n} {tuple(t.shape)} does not match acc {tuple(acc.shape)}")
+    check(load().flite_apg_euler(stream_ptr(acc.device), uncond.data_ptr(), cond.data_ptr(), acc.data_ptr(),
+                                 acc.numel(), float(guidance), float(k), float(orth_scale), float(dt)),
+          "flite_apg_euler")
+    return acc
+
+
 # ------------------------------------------------------------------------------------------------
 # MXFP8 (include/flite.h: e4m3 elements, one E8M0 scale per 32 K elements, scales [K/128][rows_pad][4])
 # ------------------------------------------------------------------------------------------------
@@ -517,6 +546,10 @@ class DitEngine:
     def enable_fp8(self, on: bool = True, device=None):
         check(self.lib.flite_dit_enable_fp8(self.h, stream_ptr(device), int(bool(on))), "flite_dit_enable_fp8")
 
+    def weights_updated(self, device=None):
+        """The bound weights changed in place: remake the engine's derived copies (fp8: requantise)."""
+        check(self.lib.flite_dit_weights_updated(self.h, stream_ptr(device)), "flite_dit_weights_updated")
+
     def set_probe(self, kind: int, max_pairs: int = 4096):
         check(self.lib.flite_dit_set_probe(self.h, kind, max_pairs), "flite_dit_set_probe")
 
@@ -587,6 +620,10 @@ class VaeEngine:
     def enable_fp8_weights(self, on: bool = True):
         """MXFP8 storage of the packed conv weights (expanded to bf16 per conv); takes effect at the next prepare."""
         check(self.lib.flite_vae_enable_fp8_weights(self.h, int(bool(on))), "flite_vae_enable_fp8_weights")
+
+    def weights_updated(self):
+        """The bound weights changed in place: re-pack (and, with fp8 storage, requantise) the conv weights."""
+        check(self.lib.flite_vae_weights_updated(self.h), "flite_vae_weights_updated")
 
     def decode_uint8(self, z, img, scaling, shift):
         require_gpu(z, "latents", torch.float32)

@@ -165,6 +165,7 @@ class DiT(nn.Module):
         self._engine = None
         self._bound = None
         self._fp8 = False
+        self._wgen = 0
 
     # ------------------------------------------------------------------ construction helpers
     @classmethod
@@ -188,6 +189,7 @@ class DiT(nn.Module):
         for name, p in self.named_parameters():
             _native.init_param_(p.data, name, seed=seed, std=std, ones=_is_norm_weight(name))
         torch.cuda.synchronize()
+        self._wgen += 1  # written through raw pointers: no version bump
         return self
 
     @property
@@ -283,16 +285,19 @@ class DiT(nn.Module):
                                      "(move the model with .to('cuda', torch.bfloat16)); there is no CPU fallback")
         if self.dtype != torch.bfloat16:
             raise _native.FliteError("the native DiT path computes with bf16 parameters; call .to(torch.bfloat16)")
-        sig = tuple((n, p.data_ptr()) for n, p in params)
+        # storage (pointers) and contents: an in-place update (load_state_dict's copy_, random_init_) bumps the
+        # version, and the engine's derived copies (fp8 weights) are remade from the new values
+        ptrs = tuple((n, p.data_ptr()) for n, p in params)
+        vers = (self._wgen,) + tuple(p._version for _, p in params)
         if self._engine is None:
             self._engine = _native.DitEngine(self._native_config())
             self._bound = None
-        if self._bound != sig:
+        if self._bound is None or self._bound[0] != ptrs:
             for n, p in params:
-                self._engine.bind(n, p.data)
-            self._bound = sig
-            if self._fp8:  # rebinding dropped the engine's fp8 copies: requantise
-                self._engine.enable_fp8(True, self.device)
+                self._engine.bind(n, p.data)  # new storage: the engine requantises before its next run
+        elif self._bound[1] != vers:
+            self._engine.weights_updated(self.device)
+        self._bound = (ptrs, vers)
         return self._engine
 
     def enable_fp8(self, enabled: bool = True):

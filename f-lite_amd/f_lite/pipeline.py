@@ -30,6 +30,17 @@ import torch
 from . import _native
 from .model import DiT
 
+# The system message of the reference's caption template (pipeline.py:106): part of the text the encoder sees,
+# so it is part of the interface.
+_SYSTEM_PROMPT = (
+    "You are a text-to-image generation model engineered to transform user-provided textual captions directly "
+    "into high-quality, visually rich image tokens. Your core objective is to generate the best possible, "
+    "highest-fidelity image that creatively interprets and expands upon the user's intent while maintaining "
+    "strong semantic alignment with the original caption. You are designed for maximum visual quality, artistic "
+    "flair, and implicit adherence to best practices in image generation (e.g., proper anatomy, clear focus, "
+    "compelling composition), ensuring a stunning visual result from even concise descriptions."
+)
+
 
 @dataclass
 class APGConfig:
@@ -104,6 +115,8 @@ class FLitePipeline:
         self._seq_parallel = False
         self._sp_group = None
         self._sp_ring = False
+        self._data_parallel = False
+        self._dp_group = None
 
     # ---------------------------------------------------------------- loading
     @classmethod
@@ -177,6 +190,21 @@ class FLitePipeline:
     def disable_cfg_parallel(self):
         self._cfg_parallel = False
 
+    def enable_data_parallel(self, group=None):
+        """One reference batch of images over every rank of `group` (no reference counterpart):
+        image i of the batch runs on rank i mod N; with APG the batch-global sums are all-reduced per step, so
+        the batch comes out as the single-GPU batched loop's. Every rank calls the pipeline with the same inputs
+        and gets every image (the final latents are all-gathered; each rank decodes the whole batch)."""
+        import torch.distributed as dist
+
+        if not (dist.is_available() and dist.is_initialized()):
+            raise ValueError("enable_data_parallel needs an initialised torch.distributed process group")
+        self._dp_group = group
+        self._data_parallel = True
+
+    def disable_data_parallel(self):
+        self._data_parallel = False
+
     def enable_sequence_parallel(self, group=None, ring: bool = False):
         """Single-image latency over every rank of `group` (no reference counterpart):
         each rank computes a slice of the token rows of every DiT launch, exchanging K/V rows per block
@@ -209,6 +237,15 @@ class FLitePipeline:
     def _execution_device(self):
         return self.dit_model.device
 
+    def _convert_caption_to_messages(self, caption: str) -> str:
+        """pipeline.py:105-124: the system + user chat messages of a caption through the processor's chat
+        template (text only, generation prompt appended)."""
+        messages = [
+            {"role": "system", "content": _SYSTEM_PROMPT},
+            {"role": "user", "content": [{"type": "text", "text": caption}]},
+        ]
+        return self.processor.apply_chat_template(messages, tokenize=False, add_generation_prompt=True)
+
     def encode_prompt(self, prompt, negative_prompt=None, device=None, dtype=None, max_sequence_length=512,
                       return_index=-8):
         """pipeline.py:126-175: hidden_states[return_index] of the text encoder over the tokenized prompts
@@ -225,7 +262,12 @@ class FLitePipeline:
             prompt = [prompt]
         enc = self.text_encoder
         device = device or enc.device
-        texts = [self.caption_to_text(p) for p in prompt] if self.caption_to_text else list(prompt)
+        if self.caption_to_text is not None:
+            texts = [self.caption_to_text(p) for p in prompt]
+        elif getattr(self.processor, "chat_template", None):  # Qwen2.5-VL & co: the reference's template
+            texts = [self._convert_caption_to_messages(p) for p in prompt]
+        else:  # T5 tokenizers have no chat template: raw captions (pt.py's T5 pipeline)
+            texts = list(prompt)
         tok = self.processor(text=texts, padding="longest", pad_to_multiple_of=8, max_length=max_sequence_length,
                              truncation=True, return_tensors="pt")
         if isinstance(enc, T5Encoder):
@@ -294,20 +336,21 @@ class FLitePipeline:
         if negative_prompt_embeds.shape[1] != L:
             raise ValueError("prompt and negative prompt embeddings must have the same length")
         if self._seq_parallel:
-            if apg_config.enabled:
-                raise NotImplementedError("APG is not available in the sequence-parallel mode")
             from .distributed import sequence_parallel_sample
 
             acc = sequence_parallel_sample(dit, latents, prompt_embeds, negative_prompt_embeds, num_inference_steps,
                                            guidance_scale, alpha, group=self._sp_group,
-                                           ring=self._sp_ring)
+                                           ring=self._sp_ring, apg=apg_config)
         elif self._cfg_parallel and do_cfg:
-            if apg_config.enabled:
-                raise NotImplementedError("APG is not available in the CFG-parallel mode")
             from .distributed import cfg_parallel_sample
 
             acc = cfg_parallel_sample(dit, latents, prompt_embeds, negative_prompt_embeds, num_inference_steps,
-                                      guidance_scale, alpha, group=self._cfg_group)
+                                      guidance_scale, alpha, group=self._cfg_group, apg=apg_config)
+        elif self._data_parallel and do_cfg:
+            from .distributed import data_parallel_sample
+
+            acc = data_parallel_sample(dit, latents, prompt_embeds, negative_prompt_embeds, num_inference_steps,
+                                       guidance_scale, alpha, group=self._dp_group, apg=apg_config)
         else:
             if do_cfg:
                 ctx = torch.cat([negative_prompt_embeds, prompt_embeds])  # uncond first (pipeline.py:266)

@@ -10,9 +10,11 @@ Differences, each one a consequence of this path's scope:
     uninitialised device memory, so running with a missing tensor would be silently wrong);
   * residual_v defaults to False: the reference's default (True) names a value-residual DiT that its own
     model.py does not accept (SURVEY §2 row 9, stale); True raises here too;
-  * LoRA (peft) and the T5 text encoder are out of scope: lora_path raises, and the pipeline
-    takes prompt_embeds; the Flux VAE is loaded from `vae_path` (a local diffusers folder) when given --
-    hub names cannot be resolved offline;
+  * LoRA (peft) is out of scope: lora_path raises. The T5 encoder and its tokenizer come from
+    `text_encoder_path` as in pt.py:147-155 (subfolders text_encoder_2 / tokenizer_2 of a local FLUX-layout
+    folder; the encoder runs natively, f_lite.text_encoder.T5Encoder); without it the pipeline takes
+    prompt_embeds. The Flux VAE is loaded from `vae_path` (a local diffusers folder) when given -- hub names
+    cannot be resolved offline, which is also why neither path defaults to "black-forest-labs/FLUX.1-schnell";
   * compile_model is a no-op: the denoise loop is already one hipGraph.
 """
 from __future__ import annotations
@@ -73,8 +75,6 @@ def load_f_lite_pt(
                                   "stale against the reference's own DiT)")
     if lora_path is not None:
         raise NotImplementedError("LoRA adapters (peft) are out of scope for the native sampling path")
-    if text_encoder_path is not None:
-        logger.warning("text_encoder_path ignored: the native path takes prompt_embeds (text encoding is §8f)")
     if dtype not in _DTYPES:
         raise ValueError(f"dtype must be one of {sorted(_DTYPES)}")
     if _DTYPES[dtype] != torch.bfloat16:
@@ -105,7 +105,12 @@ def load_f_lite_pt(
     else:
         logger.warning("no vae_path: the Flux VAE cannot be fetched offline; decode needs a VAE "
                        "(output_type='latent' works without one)")
-    pipe = FLitePipeline(dit_model=dit, vae=vae)
+    text_encoder, tokenizer = None, None
+    if text_encoder_path is not None:  # pt.py:147-155
+        text_encoder, tokenizer = load_t5_from_folder(text_encoder_path, device)
+    else:
+        logger.warning("no text_encoder_path: T5 cannot be fetched offline; pass prompt_embeds to the pipeline")
+    pipe = FLitePipeline(dit_model=dit, vae=vae, text_encoder=text_encoder, tokenizer=tokenizer)
     if enable_vae_slicing:
         pipe.enable_vae_slicing()
     if enable_vae_tiling:
@@ -113,3 +118,22 @@ def load_f_lite_pt(
     if compile_model:
         logger.info("compile_model: the native denoise loop is captured in a hipGraph already")
     return pipe
+
+
+def load_t5_from_folder(path: Union[str, Path], device):
+    """T5 encoder + tokenizer from a local FLUX-layout folder (pt.py:149-155: subfolders text_encoder_2 and
+    tokenizer_2; a folder holding config.json directly is taken as the encoder itself). The encoder runs on the
+    native path (bf16, as pt.py's torch_dtype); the tokenizer is transformers' fast tokenizer loaded offline."""
+    from .text_encoder import T5Encoder
+
+    p = Path(path)
+    enc_dir = p / "text_encoder_2" if (p / "text_encoder_2" / "config.json").exists() else p
+    text_encoder = T5Encoder.from_pretrained(enc_dir, torch_dtype=torch.bfloat16, device=device)
+    tok_dir = next((d for d in (p / "tokenizer_2", p / "tokenizer", p) if (d / "tokenizer_config.json").exists()
+                    or (d / "tokenizer.json").exists() or (d / "spiece.model").exists()), None)
+    if tok_dir is None:
+        raise FileNotFoundError(f"no tokenizer files under {p} (tokenizer_2/ as pt.py:150 expects)")
+    from transformers import AutoTokenizer
+
+    tokenizer = AutoTokenizer.from_pretrained(str(tok_dir), local_files_only=True)
+    return text_encoder, tokenizer

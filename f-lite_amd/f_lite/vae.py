@@ -137,6 +137,7 @@ class AutoencoderKL(nn.Module):
         self._engine = None
         self._bound = None
         self._prepared = None
+        self._wgen = 0  # bumped by writers that bypass the parameters' version counters
         # diffusers AutoencoderKL tiling state (enable_tiling / disable_tiling): tiles of sample_size pixels =
         # sample_size / 2**(levels-1) latents, overlap factor 0.25
         self.use_tiling = False
@@ -230,15 +231,20 @@ class AutoencoderKL(nn.Module):
         params = list(self.named_parameters())
         if not params[0][1].is_cuda or self.dtype != torch.bfloat16:
             raise _native.FliteError("the native VAE decoder needs bf16 parameters on a ROCm device")
-        sig = tuple((n, p.data_ptr()) for n, p in params)
+        # storage and contents: an in-place update (load_state_dict's copy_) bumps the parameters' versions, and
+        # the engine re-packs its conv weights from the new values
+        ptrs = tuple((n, p.data_ptr()) for n, p in params)
+        vers = (self._wgen,) + tuple(p._version for _, p in params)
         if self._engine is None:
             self._engine = _native.VaeEngine(self.config)
             self._bound = None
-        if self._bound != sig:
+        if self._bound is None or self._bound[0] != ptrs:
             for n, p in params:
                 self._engine.bind(n, p.data)
-            self._bound = sig
             self._prepared = None
+        elif self._bound[1] != vers:
+            self._engine.weights_updated()
+        self._bound = (ptrs, vers)
         if self._prepared is None:
             self._engine.enable_fp8_weights(self.fp8_weights)
         return self._engine

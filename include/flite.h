@@ -244,13 +244,33 @@ int flite_dit_sample(flite_dit* dit, void* stream, float* acc, int n_img, int n_
 int flite_cfg_euler(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
                     float dt, int use_cfg);
 /*
+ * APG (pipeline.py:276-287) on NCHW fp32 branch outputs, split at its two batch-global reductions so that
+ * ranks holding different images of one reference batch can all-reduce the partial sums in between (SURVEY §8e;
+ * the CFG-parallel mode calls them without a collective). out2 (device, 2 floats):
+ *   phase 0: [sum c (c - u), sum c^2]             -> k = sum0 / sum1 (0 if sum1 == 0)
+ *   phase 1: [sum o, sum o^2], o = (c - u) - k c  -> unbiased std s of o, orth_scale = min(1, threshold / s)
+ * flite_apg_euler: acc += dt * (c + (guidance - 1) * orth_scale * o). The sums use flite_dit_sample's APG
+ * kernel's expressions and summation order (bit-identical when one rank holds the whole batch).
+ */
+int flite_apg_sums(void* stream, const float* uncond, const float* cond, long n, float k, int phase, float* out2);
+int flite_apg_euler(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
+                    float k, float orth_scale, float dt);
+/*
  * fp8 mode (BASELINE.json configs[4]): enable=1 quantises every bound block GEMM weight (qkv, proj, cross q /
  * proj, SwiGLU gate|up, down) once into engine-owned MXFP8 copies and runs those GEMMs on the block-scaled fp8
  * MFMA with MXFP8 activations (RMSNorm+modulate, attention output and SwiGLU output quantised where they are
  * produced). Attention, norms, RoPE, the residual stream and the small GEMMs stay bf16/fp32. enable=0 returns to
- * the bf16 path. Re-binding a weight drops the fp8 copies; call again to requantise.
+ * the bf16 path. enable=1 always requantises from the weights bound now. Re-binding a weight to new storage
+ * keeps fp8 mode on: the next flite_dit_forward / flite_dit_sample requantises before it runs.
  */
 int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable);
+/*
+ * The CONTENTS of bound weights changed in place (a load_state_dict copy, a LoRA merge, re-initialisation):
+ * every engine-owned copy derived from them is remade -- in fp8 mode the MXFP8 weights are requantised on
+ * `stream` now. The bf16 path reads the bound storage directly and needs nothing. No reference counterpart
+ * (nn.Linear reads its parameters on every call).
+ */
+int flite_dit_weights_updated(flite_dit* dit, void* stream);
 
 /* ---- sequence parallelism: one image's rows over `nranks` GPUs ("ring attention over T")
  * Rank r holds rows [r*Tl, (r+1)*Tl) of every sequence, Tl = ceil(T / nranks) (T = 16 registers + patches;
@@ -317,6 +337,9 @@ int flite_vae_bind(flite_vae* vae, const char* name, const void* ptr, long numel
  * counterpart: SURVEY 8f rank 4): the packed 3x3 conv weights are kept as MXFP8 (e4m3 + one E8M0 scale per 32
  * input-channel values of a tap) and expanded to bf16 right before each conv. Takes effect at the next prepare. */
 int flite_vae_enable_fp8_weights(flite_vae* vae, int on);
+/* The CONTENTS of bound weights changed in place: re-pack (and, with fp8 storage, requantise) the engine's conv
+ * weights for the prepared shape now. */
+int flite_vae_weights_updated(flite_vae* vae);
 int flite_vae_prepare(flite_vae* vae, int latent_h, int latent_w);
 /* latents fp32 [n_img, C, h, w] -> images uint8 [n_img, 8h, 8w, 3] (device), decoding z/scaling + shift. */
 int flite_vae_decode_uint8(flite_vae* vae, void* stream, const float* latents, int n_img, void* images,

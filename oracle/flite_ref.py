@@ -331,11 +331,13 @@ class APG:
 
 
 def sample(dit, latents, prompt_embeds, negative_embeds, num_steps=30, guidance_scale=6.0, alpha=None,
-           apg: Optional[APG] = None, t_dtype=None, acc_dtype=None, height=None, width=None, trace=None):
+           apg: Optional[APG] = None, t_dtype=None, acc_dtype=None, height=None, width=None, trace=None,
+           max_steps=None):
     """The denoise loop of FLitePipeline.__call__ (pipeline.py:245-297). Returns the final latents.
 
     t_dtype: dtype of the timestep tensor (pipeline.py:260 uses the model dtype: bf16 in a bf16 model).
     acc_dtype: dtype of the Euler accumulator (reference: the model dtype).
+    max_steps: stop after this many steps of the num_steps schedule (timing samples only).
     """
     B = latents.shape[0]
     lh, lw = latents.shape[-2:]
@@ -348,6 +350,8 @@ def sample(dit, latents, prompt_embeds, negative_embeds, num_steps=30, guidance_
     cfg = guidance_scale >= 1.0
     apg = apg or APG(enabled=False)
     for step, (t, dt) in enumerate(schedule(num_steps, height, width, alpha)):
+        if max_steps is not None and step >= max_steps:
+            break
         tt = torch.tensor([t] * B, dtype=t_dtype)
         if cfg:
             out = dit(torch.cat([lat] * 2), torch.cat([negative_embeds, prompt_embeds]), None, torch.cat([tt] * 2))

@@ -27,3 +27,11 @@ def golden_meta():
     import json
 
     return json.loads((ROOT / "tests" / "golden" / "golden_meta.json").read_text())
+
+
+@pytest.fixture(scope="session")
+def golden_nobias():
+    """Reference outputs of the released-checkpoint layout (train_bias_and_rms=False, pt.py:31)."""
+    from safetensors.torch import load_file
+
+    return load_file(str(ROOT / "tests" / "golden" / "golden_nobias.safetensors"))

@@ -165,3 +165,73 @@ def test_sharding_and_broadcast(world):
         assert t == float(world)  # slowest rank's time
         shards += mine
     assert sorted(shards) == list(range(8))  # every image exactly once
+
+
+def _dp_apg_worker(rank, world, port, q):
+    """One rank of the data-parallel loop with APG: its images of the batch, the branch forward by the fp32
+    oracle (test infrastructure), APG's sums all-reduced between the two phases (distributed.apg_step)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from f_lite.distributed import all_reduce_sum_, apg_step, data_parallel_loop, gather_images, image_indices
+    from oracle import flite_ref as R
+
+    lat, pos, neg = _dp_inputs()
+    mine = image_indices(lat.shape[0], rank, world)
+    ref = R.RefDiT.random(R.PRESETS["tiny"], dtype=torch.float32)
+    sched = R.schedule(4, 128, 128)
+    ctx = torch.cat([neg[mine], pos[mine]])
+
+    def forward_pair(x, i):
+        out = ref(torch.cat([x, x]), ctx, None, torch.tensor([sched[i][0]] * 2 * x.shape[0]))
+        return out.chunk(2)
+
+    def sums(u, c, k, phase):
+        if phase == 0:
+            return torch.stack([(c * (c - u)).sum(), (c * c).sum()])
+        o = (c - u) - k * c
+        return torch.stack([o.sum(), (o * o).sum()])
+
+    def update(a, u, c, gs, k, sc, dt):
+        a += dt * (c + (gs - 1) * sc * ((c - u) - k * c))
+
+    n_total = lat.numel()
+
+    def combine(x, u, c, dt):
+        apg_step(x, u, c, dt, 6.0, 0.03, n_total, sums, update, reduce=all_reduce_sum_)
+
+    acc = data_parallel_loop(lat[mine].clone(), [dt for _, dt in sched], forward_pair, combine)
+    q.put((rank, gather_images(acc, lat.shape[0])))
+    dist.destroy_process_group()
+
+
+def _dp_inputs():
+    g = torch.Generator().manual_seed(12)
+    lat = torch.randn(3, 16, 16, 16, generator=g)
+    pos = torch.randn(3, 24, 128, generator=g)
+    neg = torch.randn(3, 24, 128, generator=g)
+    return lat, pos, neg
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_data_parallel_apg_matches_batched_oracle(world):
+    """SURVEY §8e: one reference batch (3 images) sharded over the ranks (image i -> rank i mod N) with APG on;
+    the batch-global sums are all-reduced twice per step, and every rank ends with the batched APG loop's
+    latents (pipeline.py:250-297, fp32 oracle)."""
+    from oracle import flite_ref as R
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_apg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    for r in range(1, world):
+        assert torch.equal(res[0], res[r])
+    lat, pos, neg = _dp_inputs()
+    ref = R.sample(R.RefDiT.random(R.PRESETS["tiny"], dtype=torch.float32), lat, pos, neg, num_steps=4,
+                   guidance_scale=6.0, apg=R.APG(enabled=True), height=128, width=128, t_dtype=torch.float32,
+                   acc_dtype=torch.float32)
+    assert torch.allclose(res[0], ref, rtol=1e-4, atol=1e-4), (res[0] - ref).abs().max()

@@ -194,8 +194,40 @@ def test_dit_fp8_sampling_loop_graph_equals_eager(golden):
     assert torch.equal(run[0], run[1]) and torch.equal(run[1], run[2])
 
 
+@pytest.mark.parametrize("depth", [1, 2])
+def test_10b_fp8_full_width_vs_fake_quant_oracle(depth):
+    """configs[4] at full width: the 10B layout at the reference's default 1344x896 (T = 4720, 112-row attention
+    tails), a 512-token context, depth 1-2, fp8 mode vs the fake-quant oracle (RefDiT(fp8=True): the same MXFP8
+    rounding at the same points of the fp32 forward). Covers the shapes the 512-wide presets never reach: the
+    gate/up interleave at F = 12288, the SwiGLU -> e4m3 epilogue of full-size tiles, the attention's MXFP8
+    output at the T = 4720 tails, the 224-row tiles. Also reports MXFP8's intrinsic cost (fake-quant oracle vs
+    the fp32 oracle) and the bf16 path's distance at the same shape."""
+    import dataclasses
+
+    cfg = dict(PRESETS["10b"], depth=depth)
+    m = DiT.random(seed=0, device=DEV, **cfg)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 16, 112, 168, generator=g).bfloat16()
+    ctx = torch.randn(2, 512, 4096, generator=g).bfloat16()
+    t = torch.tensor([0.75, 0.75]).bfloat16()
+    bf = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32).cpu()
+    m.enable_fp8(True)
+    f8 = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32).cpu()
+    rc = dataclasses.replace(R.PRESETS["10b"], depth=depth)
+    with torch.no_grad():
+        fq = R.RefDiT.random(rc, dtype=torch.float32, fp8=True)(x.float(), ctx.float(), None, t)
+        f32 = R.RefDiT.random(rc, dtype=torch.float32)(x.float(), ctx.float(), None, t)
+    p_fq, p_32, p_bf, p_int = psnr(f8, fq), psnr(f8, f32), psnr(bf, f32), psnr(fq, f32)
+    print(f"10B 1344x896 depth {depth} fp8: {p_fq:.2f} dB vs fake-quant oracle, {p_32:.2f} dB vs fp32 oracle; "
+          f"MXFP8 intrinsic (fake-quant vs fp32 oracle) {p_int:.2f} dB; bf16 path vs fp32 oracle {p_bf:.2f} dB; "
+          f"fp8 vs bf16 path {psnr(f8, bf):.2f} dB")
+    assert p_fq >= 30.0
+
+
 def test_10b_fp8_full_size_forward():
-    """The configs[4] model at the reference's default 1344x896 (T = 4720), full depth: fp8 vs the bf16 path."""
+    """The configs[4] model at the reference's default 1344x896 (T = 4720), full depth: fp8 vs the bf16 path.
+    The bar sits 3 dB under the measured value (24.98 dB, round 2): the distance is MXFP8's own cost compounded
+    over 40 blocks (tools/fp8_depth_decay.py measures it against the fake-quant and fp32 oracles by depth)."""
     m = DiT.random(seed=0, device=DEV, **PRESETS["10b"])
     g = torch.Generator().manual_seed(5)
     x = torch.randn(2, 16, 112, 168, generator=g).bfloat16().to(DEV)
@@ -208,7 +240,7 @@ def test_10b_fp8_full_size_forward():
     assert torch.isfinite(f8).all() and torch.equal(f8, f8b)
     p = psnr(f8, bf)
     print(f"10B 1344x896 full-depth forward: fp8 vs bf16 path {p:.2f} dB")
-    assert p > 15.0
+    assert p > 22.0
 
 
 @pytest.mark.parametrize("preset,hw", [("tiny", (16, 16)), ("10b_d2", (112, 168))])

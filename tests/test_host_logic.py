@@ -145,3 +145,96 @@ def test_vae_tiling_flags():
     assert not vae.use_tiling
     FLitePipeline(None, vae).enable_vae_tiling()  # pipeline.py:90-93 forwards to the VAE
     assert vae.use_tiling
+
+
+class _ChatProcessor:
+    """A processor with a chat template (Qwen2.5-VL's AutoProcessor shape): records what it is asked to render
+    and tokenize."""
+
+    chat_template = "{{ messages }}"
+
+    def __init__(self):
+        self.rendered = []
+
+    def apply_chat_template(self, messages, tokenize=False, add_generation_prompt=False):
+        assert tokenize is False and add_generation_prompt is True
+        self.rendered.append(messages)
+        return "<chat>" + messages[0]["content"][:16] + "|" + messages[1]["content"][0]["text"] + "</chat>"
+
+    def __call__(self, text=None, **kw):
+        self.texts = list(text)
+        n = max(len(t) for t in text)
+        return {"input_ids": torch.ones(len(text), n, dtype=torch.long),
+                "attention_mask": torch.ones(len(text), n, dtype=torch.long)}
+
+
+class _HiddenStatesEncoder(torch.nn.Module):
+    """Stands in for a transformers encoder called the reference's way (pipeline.py:148-154)."""
+
+    def __init__(self):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.zeros(1))
+
+    @property
+    def device(self):
+        return torch.device("cpu")
+
+    def forward(self, input_ids=None, attention_mask=None, use_cache=False, return_dict=True,
+                output_hidden_states=True):
+        from types import SimpleNamespace
+
+        h = input_ids.float()[..., None].expand(-1, -1, 8)
+        return SimpleNamespace(hidden_states=[h] * 9)
+
+
+def test_encode_prompt_applies_reference_chat_template():
+    """pipeline.py:105-124,139-142: a processor with a chat template gets the reference's system + user messages
+    for every caption (negative prompts too); the rendered strings are what gets tokenized."""
+    import re
+
+    from f_lite.pipeline import _SYSTEM_PROMPT
+
+    proc = _ChatProcessor()
+    p = FLitePipeline(DiT(**PRESETS["tiny"]), text_encoder=_HiddenStatesEncoder(), processor=proc)
+    pos, neg = p.encode_prompt(["a cat", "a dog"], negative_prompt="blurry", dtype=torch.float32)
+    assert pos.shape[0] == 2 and neg.shape[0] == 1
+    assert [m[1]["content"][0]["text"] for m in proc.rendered] == ["a cat", "a dog", "blurry"]
+    for m in proc.rendered:
+        assert m[0] == {"role": "system", "content": _SYSTEM_PROMPT}
+        assert m[1]["role"] == "user" and m[1]["content"][0]["type"] == "text"
+    assert proc.texts == ["<chat>" + _SYSTEM_PROMPT[:16] + "|blurry</chat>"]
+    # the system prompt is the reference's text, character for character
+    src = open("/root/reference/f_lite/pipeline.py").read() if __import__("os").path.exists(
+        "/root/reference/f_lite/pipeline.py") else None
+    if src is not None:
+        assert re.search(r'system_prompt = "(.*?)"\n', src).group(1) == _SYSTEM_PROMPT
+    # an explicit caption_to_text hook wins over the template
+    p.caption_to_text = lambda c: "raw:" + c
+    p.encode_prompt("x", dtype=torch.float32)
+    assert proc.texts == ["raw:x"]
+
+
+def test_apg_step_scalar_algebra_matches_reference():
+    """distributed.apg_step (the two-phase APG used by the CFG-parallel and data-parallel modes) with torch sums
+    equals pipeline.py:276-287's whole-batch APG on the same branch outputs."""
+    from f_lite.distributed import apg_step
+
+    g = torch.Generator().manual_seed(3)
+    u = torch.randn(3, 16, 8, 8, generator=g)
+    c = u + 0.3 * torch.randn(3, 16, 8, 8, generator=g)
+    acc = torch.randn(3, 16, 8, 8, generator=g)
+
+    def sums(u_, c_, k, phase):
+        if phase == 0:
+            return torch.stack([(c_ * (c_ - u_)).sum(), (c_ * c_).sum()])
+        o = (c_ - u_) - k * c_
+        return torch.stack([o.sum(), (o * o).sum()])
+
+    def update(a, u_, c_, gs, k, sc, dt):
+        a += dt * (c_ + (gs - 1) * sc * ((c_ - u_) - k * c_))
+
+    got = apg_step(acc.clone(), u, c, 0.1, 6.0, 0.03, u.numel(), sums, update)
+    dy, dd = c, c - u
+    orth = dd - (dy * dd).sum() / (dy * dy).sum() * dy
+    want = acc + 0.1 * (dy + 5.0 * orth * min(1, 0.03 / orth.std()))
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)

@@ -96,3 +96,17 @@ def test_generator_deterministic():
     assert torch.equal(w, b["blocks.0.self_attn.qkv.weight"])
     assert abs(w.std().item() - 0.02) < 1e-3 and abs(w.mean().item()) < 1e-3
     assert torch.equal(w, w.bfloat16().float())
+
+
+@pytest.mark.parametrize("preset,key,mask", [("tiny", "tiny", False), ("tiny", "tiny", True),
+                                             ("tiny_v2", "tiny_v2", False)])
+def test_dit_released_layout_fp32(golden, golden_nobias, preset, key, mask):
+    """train_bias_and_rms=False (the layout pt.py:31 loads): no qkv / q / context_kv biases (model.py:465) and
+    a weight-less final RMSNorm (model.py:474), pinned to the stub-loaded reference (make_golden_nobias.py)."""
+    import dataclasses
+
+    cfg = dataclasses.replace(R.PRESETS[preset], train_bias_and_rms=False)
+    d = R.RefDiT.random(cfg, dtype=torch.float32)
+    assert "final_norm.weight" not in d.p and not any(k.endswith("qkv.bias") for k in d.p)
+    out = d(golden["in.x"], golden["in.ctx"], golden["in.mask"] if mask else None, golden["in.t"])
+    assert rel(out, golden_nobias[f"dit.{key}.nobias.f32.{'mask' if mask else 'nomask'}"]) < 2e-5
