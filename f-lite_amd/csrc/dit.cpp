@@ -30,6 +30,12 @@ bool w_prefetch() {
   return on;
 }
 
+// the norm2 pass reading the cross-q weights ahead (NormModParams::pf); FLITE_NO_NORM_PF=1 turns only it off
+bool norm_prefetch() {
+  static const bool on = w_prefetch() && getenv("FLITE_NO_NORM_PF") == nullptr;
+  return on;
+}
+
 bool parse_block(const std::string& name, int* idx, std::string* rest) {
   if (name.rfind("blocks.", 0) != 0) return false;
   const size_t dot = name.find('.', 7);
@@ -483,7 +489,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   auto norm = [&](const bf16_t* w, const float* sh, const float* sc, const bf16_t* pf0 = nullptr, long pf0_n = 0,
                   const bf16_t* pf1 = nullptr, long pf1_n = 0) -> int {
     NormModParams nm;
-    if (w_prefetch()) {
+    if (norm_prefetch()) {
       nm.pf[0] = pf0;
       nm.pf_bytes[0] = pf0_n * 2;
       nm.pf[1] = pf1;

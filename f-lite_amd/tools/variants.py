@@ -59,7 +59,7 @@ def build(src, name, args):
         raise RuntimeError(r.stderr[-4000:])
     objs = [str(obj)] + [str(bn.BUILD / (p.stem + ".o")) for p in bn._sources() if p.stem != src]
     subprocess.run([bn.HIPCC, f"--offload-arch={bn.ARCH}", "-shared", "-fPIC", "-o", str(out / "libflite_hip.so"),
-                    *objs], check=True)
+                    *objs, "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"], check=True)
     (out / "defines.json").write_text(json.dumps({"defines": defines, "subs": subs}))
     print(f"built variant {name}: {defines} {len(subs)} substitution(s)")
 
@@ -98,7 +98,28 @@ def time_gemms(iters=20):
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / iters
-        res[name] = (ms, 2.0 * M * N * K / ms / 1e9)
+        err = None
+        if os.environ.get("VARIANTS_CHECK"):  # one launch against torch's fp32 product of the same operands
+            af = a.float()
+            if epi == "swiglu":
+                ref = torch.nn.functional.silu(af @ w.float().t()) * (af @ w2.float().t())
+                o = torch.empty_like(out)
+                nat.gemm(a, w, out=o, workspace=ws, **kw)
+            elif epi == "resid":
+                x0 = torch.randn(M, N, device="cuda")
+                g = kw["gate"]
+                seg = (torch.arange(M, device="cuda") // (M // 2)).clamp(max=1)
+                ref = x0 + (af @ w.float().t()) * g[seg]
+                o = x0.clone()
+                nat.gemm(a, w, out=o, workspace=ws, **kw)
+            else:
+                ref = af @ w.float().t()
+                o = torch.empty_like(out)
+                nat.gemm(a, w, out=o, workspace=ws, **kw)
+            torch.cuda.synchronize()
+            err = ((o.float() - ref).norm() / ref.norm()).item()
+            del ref, o
+        res[name] = (ms, 2.0 * M * N * K / ms / 1e9, err)
     return res
 
 
@@ -161,8 +182,9 @@ def main():
                 print(p.stdout[-2000:], p.stderr[-2000:])
                 sys.exit(1)
             table[n].append(json.loads(line[0][7:]))
-            print(f"round {r} {n}: " + " ".join(f"{k} {v[0]*1e3:.1f}us/{v[1]:.0f}TF" for k, v in table[n][-1].items()),
-                  flush=True)
+            print(f"round {r} {n}: " + " ".join(f"{k} {v[0]*1e3:.1f}us/{v[1]:.0f}TF" +
+                                                 (f"/err {v[2]:.1e}" if len(v) > 2 and v[2] is not None else "")
+                                                 for k, v in table[n][-1].items()), flush=True)
     print("== median us per shape")
     for n in names:
         shapes = table[n][0].keys()

@@ -146,3 +146,61 @@ def test_10b_1024_30_steps_graph_eager_deterministic(m10b):
     assert torch.isfinite(a).all()
     assert a.abs().max() > 0.1 and a.std() > 0.1
     assert torch.equal(a, b) and torch.equal(a, c)
+
+
+# ---- SURVEY §8c fixture set (iv) / §8d "re-measure P2 at T = 4112" (tests/golden/make_golden_full2.py) ----
+@pytest.fixture(scope="module")
+def gold2():
+    from safetensors.torch import load_file
+
+    f = GOLD / "golden_full2.safetensors"
+    if not f.exists():
+        pytest.skip("golden_full2.safetensors not generated")
+    return load_file(str(f)), json.loads((GOLD / "golden_full2_meta.json").read_text())
+
+
+def _teacher_input(meta, t):
+    """x_t = bf16(t * noise + (1 - t) * x0) in fp32 arithmetic, as make_golden_full2.teacher_input."""
+    noise = hashed(meta, "latents_1024").float().cpu()
+    x0 = hashed(meta, "x0_1024").float().cpu()
+    return (noise * t + x0 * (1.0 - t)).to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("name", ["7b", "10b"])
+@pytest.mark.parametrize("t", [1.0, 0.5, 0.1])
+def test_1024_teacher_forced_step(gold2, m7b, m10b, name, t):
+    """P2 at T = 4112: the CFG-batched raw output on the reference's input at t, >= 40 dB per branch; the
+    CFG-6-combined output is reported (the reference's own bf16 run sits at 38-40 dB there at 256^2)."""
+    g, meta = gold2
+    key = f"{name}.1024.tf{t}.out"
+    if key not in g:
+        pytest.skip(f"{key} not in the fixture file")
+    model = m7b if name == "7b" else m10b
+    x = _teacher_input(meta, t)
+    out = _cfg_forward(model, torch.cat([x, x]), hashed(meta, "ctx"), torch.tensor([t, t]).to(torch.bfloat16))
+    ref = g[key]
+    _check_branches(out, ref, f"{name} 1024^2 teacher-forced t={t}")
+    comb = out[0] + 6.0 * (out[1] - out[0])
+    comb_ref = ref[0] + 6.0 * (ref[1] - ref[0])
+    print(f"  CFG-6 combined output: {psnr(comb, comb_ref):.2f} dB")
+
+
+@pytest.mark.parametrize("name", ["7b", "10b"])
+def test_1024_free_running_4_steps(gold2, m7b, m10b, name):
+    """P3 at 1024^2: the native 4-step CFG-6 pipeline's final latents vs the reference's fp32 ones, beside (and
+    above) the reference's own bf16 run on the same trajectory."""
+    g, meta = gold2
+    key = f"{name}.1024.f32.final"
+    if key not in g:
+        pytest.skip(f"{key} not in the fixture file")
+    model = m7b if name == "7b" else m10b
+    pos = hashed(meta, "ctx")
+    lat = hashed(meta, "latents_1024")
+    out = FLitePipeline(model)(prompt_embeds=pos, latents=lat, height=1024, width=1024, num_inference_steps=4,
+                               guidance_scale=6.0, output_type="latent").images.float()
+    got = out / SCALING + SHIFT
+    p = psnr(got, g[key])
+    floor = meta[f"{name}.1024.bf16_vs_f32_psnr"]
+    print(f"{name} 1024^2 4-step CFG-6 final latents: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
+          f"{floor:.2f} dB)")
+    assert p >= floor
