@@ -183,6 +183,16 @@ def cpu_baseline_full(model, vae, cfg: dict, H: int, W: int, steps: int, k_steps
     rcfg = R.DiTConfig(**{k: cfg[k] for k in ("in_channels", "patch_size", "hidden_size", "depth", "num_heads",
                                                  "mlp_ratio", "cross_attn_input_size", "train_bias_and_rms",
                                                  "per_block_adaln")})
+    import threading
+
+    stop = threading.Event()
+
+    def heartbeat():  # minutes of silent CPU work: keep the log moving
+        t0 = time.time()
+        while not stop.wait(30.0):
+            print(f"[cpu baseline] {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     params = {n: t.detach().float().cpu() for n, t in model.named_parameters()}
     ref = R.RefDiT(rcfg, params, dtype=torch.float32)
     g = torch.Generator().manual_seed(0)
@@ -200,6 +210,7 @@ def cpu_baseline_full(model, vae, cfg: dict, H: int, W: int, steps: int, k_steps
             t0 = time.perf_counter()
             VR.decode_to_uint8(dec, lat)
             res["vae_s"] = time.perf_counter() - t0
+    stop.set()
     torch.set_num_threads(prev_threads)
     per_image = res["dit_steps_s"] * steps / k_steps + res["vae_s"]
     return {

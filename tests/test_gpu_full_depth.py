@@ -204,3 +204,28 @@ def test_1024_free_running_4_steps(gold2, m7b, m10b, name):
     print(f"{name} 1024^2 4-step CFG-6 final latents: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
           f"{floor:.2f} dB)")
     assert p >= floor
+
+
+def test_10b_1344x896_30_steps_tiled_vae(m10b):
+    """BASELINE configs[2] at full size: 10B layout, the reference's generate.py default 1344x896 (T = 4720),
+    30 CFG-6 steps, then the diffusers tiled decode that generate.py:77-78 turns on (112 x 168 latents exceed the
+    128-latent tile) to uint8. Finite; hipGraph replay == eager bit for bit; the whole image bit-reproducible
+    (the tiled decode's parity against the oracle at this grid: test_gpu_vae.py::test_vae_decode_tiled_default_grid)."""
+    from f_lite.vae import AutoencoderKL
+
+    ctx = torch.empty(1, 512, 4096, device=DEV, dtype=torch.bfloat16)
+    _native.init_param_(ctx, "synthetic.t5_context", seed=1, std=1.0)
+    lat = torch.empty(1, 16, 112, 168, device=DEV, dtype=torch.bfloat16)
+    _native.init_param_(lat, "synthetic.latents.0", seed=2, std=1.0)
+    pipe = FLitePipeline(m10b, vae=AutoencoderKL.random(seed=0))
+    pipe.enable_vae_tiling()
+    kw = dict(prompt_embeds=ctx, latents=lat, height=896, width=1344, num_inference_steps=30, guidance_scale=6.0)
+    a = pipe(**kw, output_type="latent", use_graph=True).images.float().cpu()
+    b = pipe(**kw, output_type="latent", use_graph=False).images.float().cpu()
+    assert torch.isfinite(a).all() and a.std() > 0.1
+    assert torch.equal(a, b)
+    img = pipe(**kw, output_type="uint8").images
+    assert img.shape == (1, 896, 1344, 3) and img.dtype == torch.uint8
+    img2 = pipe(**kw, output_type="uint8").images
+    assert torch.equal(img, img2)
+    assert img.float().std() > 1.0  # a non-degenerate picture
