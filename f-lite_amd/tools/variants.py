@@ -130,7 +130,8 @@ def time_attn(iters=30):
     torch.manual_seed(0)
     res = {}
     B, H, D = 2, 12, 256
-    for name, T, Lk in (("self", 4112, 4112), ("cross", 4112, 512), ("cross_notail", 4096, 512)):
+    for name, T, Lk in (("self", 4112, 4112), ("cross", 4112, 512), ("cross_notail", 4096, 512),
+                        ("cross_4720", 4720, 512)):
         q = torch.nn.functional.normalize(torch.randn(B * T, H, D, device="cuda"), dim=-1).mul(16).bfloat16()
         k = torch.nn.functional.normalize(torch.randn(B * Lk, H, D, device="cuda"), dim=-1).mul(16).bfloat16()
         v = torch.randn(B * Lk, H, D, device="cuda").bfloat16()
@@ -151,7 +152,19 @@ def time_attn(iters=30):
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / iters
-        res[name] = (ms, 4.0 * B * H * T * Lk * D / ms / 1e9)
+        err = None
+        if os.environ.get("VARIANTS_CHECK"):  # one launch against torch's fp32 softmax attention, 4 heads per sequence
+            o = torch.zeros_like(out)
+            nat.attn_varlen(q, k, v, cu_q, cu_k, T, D ** -0.5, out=o, max_score=16.5, workspace=ws, max_k=Lk)
+            num = den = 0.0
+            for b in range(B):
+                for h in (0, 5, 7, 11):
+                    qs, ks = q[b * T:(b + 1) * T, h].float(), k[b * Lk:(b + 1) * Lk, h].float()
+                    ref = torch.softmax(qs @ ks.t() * D ** -0.5, dim=-1) @ v[b * Lk:(b + 1) * Lk, h].float()
+                    num += (o[b * T:(b + 1) * T, h].float() - ref).norm().item() ** 2
+                    den += ref.norm().item() ** 2
+            err = (num / den) ** 0.5
+        res[name] = (ms, 4.0 * B * H * T * Lk * D / ms / 1e9, err)
     return res
 
 
@@ -172,9 +185,12 @@ def main():
     names = args
     table = {n: [] for n in names}
     for r in range(rounds):
-        for n in names:
-            lib = HERE / "variants" / n / "libflite_hip.so"
+        for n in names:  # NAME or NAME:VAR=VALUE (the variant's library under an extra environment variable)
+            lib = HERE / "variants" / n.split(":")[0] / "libflite_hip.so"
             env = dict(os.environ, FLITE_LIB=str(lib))
+            if ":" in n:
+                key, val = n.split(":", 1)[1].split("=", 1)
+                env[key] = val
             p = subprocess.run([sys.executable, __file__, "child", src], env=env, capture_output=True, text=True,
                                timeout=300)
             line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
