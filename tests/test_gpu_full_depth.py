@@ -229,3 +229,37 @@ def test_10b_1344x896_30_steps_tiled_vae(m10b):
     img2 = pipe(**kw, output_type="uint8").images
     assert torch.equal(img, img2)
     assert img.float().std() > 1.0  # a non-degenerate picture
+
+
+# ---- P3 at the metric's 30 steps, CFG 6 and CFG 1 (tests/golden/make_golden_full3.py) ----
+@pytest.fixture(scope="module")
+def gold3():
+    from safetensors.torch import load_file
+
+    f = GOLD / "golden_full3.safetensors"
+    if not f.exists():
+        pytest.skip("golden_full3.safetensors not generated")
+    return load_file(str(f)), json.loads((GOLD / "golden_full3_meta.json").read_text())
+
+
+@pytest.mark.parametrize("name", ["7b", "10b"])
+@pytest.mark.parametrize("g", [6.0, 1.0])
+def test_256_free_running_30_steps(gold3, m7b, m10b, name, g):
+    """P3 over the full 30-step schedule at 256^2: the native pipeline's final latents vs the reference's fp32
+    trajectory, beside (and above) the reference's own bf16 run; at CFG 1, where the CFG-6 noise amplification
+    is absent, the SURVEY §8d bar of 40 dB applies as stated."""
+    gd, meta = gold3
+    key = f"{name}.256.s30.g{g:g}"
+    if f"{key}.f32.final" not in gd:
+        pytest.skip(f"{key} not in the fixture file")
+    model = m7b if name == "7b" else m10b
+    out = FLitePipeline(model)(prompt_embeds=hashed(meta, "ctx"), latents=hashed(meta, "latents_256"), height=256,
+                               width=256, num_inference_steps=30, guidance_scale=g,
+                               output_type="latent").images.float()
+    p = psnr(out / SCALING + SHIFT, gd[f"{key}.f32.final"])
+    floor = meta[f"{key}.bf16_vs_f32_psnr"]
+    print(f"{name} 256^2 30-step CFG-{g:g} final latents: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
+          f"{floor:.2f} dB)")
+    assert p >= floor
+    if g == 1.0:
+        assert p >= 40.0
