@@ -273,13 +273,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required")
+    # FLITE_BENCH_REHEARSAL=1: rehearse the N-rank path on a box with fewer GPUs (ranks share GPUs round-robin,
+    # gloo instead of RCCL, which refuses two ranks on one device). Never the measured configuration: the line
+    # says so in "distributed".
+    rehearsal = world > 1 and os.environ.get("FLITE_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
@@ -403,7 +412,7 @@ def main():
             except Exception:
                 pass
     cpu = None
-    if not args.no_cpu_baseline:  # rank 0 only (the other ranks have returned), at every N
+    if not args.no_cpu_baseline and world == 1:  # at N = 1 only (rank 0)
         if args.cpu_baseline_full > 0:
             cpu = cpu_baseline_full(model, vae, cfg, args.height, args.width, args.sample_steps,
                                     args.cpu_baseline_full)
@@ -435,7 +444,10 @@ def main():
             "VAE decode to uint8" if vae is not None else "latents only (no VAE)"),
                    "images_per_gpu_per_step": BI, "cfg_batch": 2, "parallelism": "replica dp%d" % world,
                    "hipgraph": not args.no_graph, "vae_tiling": bool(args.vae_tiling)},
-        "distributed": {"world_size": world, "backend": "nccl (RCCL over xGMI)" if world > 1 else "none",
+        "distributed": {"world_size": world,
+                        "backend": ("gloo REHEARSAL (ranks share %d GPU(s); not a measurement)"
+                                    % torch.cuda.device_count() if rehearsal else
+                                    "nccl (RCCL over xGMI)" if world > 1 else "none"),
                         "collectives": "one broadcast of the [1,512,4096] context from rank 0 before the loop",
                         "images_per_rank": args.steps},
         "mfma_util_image": round(f_image * value / world / PEAK_BF16, 4),

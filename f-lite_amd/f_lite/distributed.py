@@ -396,6 +396,8 @@ def max_over_ranks(seconds: float, device=None, group=None) -> float:
 
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return seconds
+    if dist.get_backend(group) == "gloo":
+        device = "cpu"  # CPU tests / ranks sharing a GPU
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
