@@ -244,6 +244,25 @@ class DiT(nn.Module):
             sd.update(load_file(str(f)))
         return cls.from_state_dict(clean_state_dict(sd), device=device, torch_dtype=torch_dtype, **cfg)
 
+    # ------------------------------------------------------------------ LoRA (model.py:487-495; f_lite/lora.py)
+    def load_lora_weights(self, load_directory, target_modules=None):
+        """`<load_directory>/lora_weights.pt` (a peft LoRA state dict, read with weights_only=True) folded into
+        the weights: W <- W + B @ A (the adapter's lora_alpha / r = 1 as pt.py:116-121 configures it)."""
+        from .lora import merge_lora_
+
+        sd = torch.load(str(Path(load_directory) / "lora_weights.pt"), map_location="cpu", weights_only=True)
+        n = merge_lora_(self, sd, scaling=1.0, target_modules=target_modules)
+        self._lora_state_dict = sd
+        return n
+
+    def save_lora_weights(self, save_directory):
+        """`<save_directory>/lora_weights.pt`: the adapter last merged by load_lora_weights / load_f_lite_pt (the
+        weights hold it merged, so there is no separate adapter to read back, unlike the reference's peft one)."""
+        sd = getattr(self, "_lora_state_dict", None)
+        if sd is None:
+            raise RuntimeError("no LoRA adapter has been loaded into this model")
+        torch.save(sd, f"{save_directory}/lora_weights.pt")
+
     @classmethod
     def from_state_dict(cls, sd, device="cuda", torch_dtype=torch.bfloat16, **cfg):
         """Build on `device` in `torch_dtype` and load `sd` strictly. A per-block-adaLN state dict given to the

@@ -10,7 +10,9 @@ Differences, each one a consequence of this path's scope:
     uninitialised device memory, so running with a missing tensor would be silently wrong);
   * residual_v defaults to False: the reference's default (True) names a value-residual DiT that its own
     model.py does not accept (SURVEY §2 row 9, stale); True raises here too;
-  * LoRA (peft) is out of scope: lora_path raises. The T5 encoder and its tokenizer come from
+  * a LoRA adapter (lora_path, pt.py:107-135) is folded into the weights (f_lite/lora.py) instead of kept as
+    unmerged peft modules: same function, the native GEMMs unchanged. As in the reference, the adapter's scaling
+    is lora_alpha / r = 1 and lora_scale is not applied (pt.py:130 only logs it). The T5 encoder and its tokenizer come from
     `text_encoder_path` as in pt.py:147-155 (subfolders text_encoder_2 / tokenizer_2 of a local FLUX-layout
     folder; the encoder runs natively, f_lite.text_encoder.T5Encoder); without it the pipeline takes
     prompt_embeds. The Flux VAE is loaded from `vae_path` (a local diffusers folder) when given -- hub names
@@ -73,8 +75,6 @@ def load_f_lite_pt(
     if residual_v:
         raise NotImplementedError("residual_v=True: the value-residual DiT is not in f_lite/model.py (pt.py:93 is "
                                   "stale against the reference's own DiT)")
-    if lora_path is not None:
-        raise NotImplementedError("LoRA adapters (peft) are out of scope for the native sampling path")
     if dtype not in _DTYPES:
         raise ValueError(f"dtype must be one of {sorted(_DTYPES)}")
     if _DTYPES[dtype] != torch.bfloat16:
@@ -96,6 +96,14 @@ def load_f_lite_pt(
         logger.warning("ignoring %d unexpected keys, e.g. %s", len(unexpected), unexpected[:4])
         sd = {k: v for k, v in sd.items() if k in expected}
     dit = DiT.from_state_dict(sd, device=device, torch_dtype=torch.bfloat16, **cfg)
+    if lora_path is not None:  # pt.py:107-135
+        from .lora import merge_lora_
+
+        logger.info("Loading LoRA weights from %s", lora_path)
+        lsd = torch.load(str(lora_path), map_location="cpu", weights_only=True)
+        merge_lora_(dit, lsd, scaling=1.0, target_modules=lora_target_modules.split(","), rank=lora_rank)
+        dit._lora_state_dict = lsd
+        logger.info("Successfully loaded LoRA weights with scale %s", lora_scale)
     vae = None
     if vae_path is not None:
         from .vae import AutoencoderKL

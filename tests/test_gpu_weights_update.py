@@ -102,3 +102,36 @@ def test_vae_load_state_dict_in_place(fp8):
     want = make(1).decode_to_uint8(lat).cpu()
     assert not torch.equal(before, after)
     assert torch.equal(after, want)
+
+
+@pytest.mark.parametrize("preset", ["tiny", "tiny_v2"])
+def test_lora_merged_forward_matches_oracle(preset):
+    """LoRA (pt.py:107-135 / model.py:492-495, merged by f_lite/lora.py) on a model that has already run: the
+    in-place merge rebinds the engine (its cross-attention K/V cache included) and the forward matches the fp32
+    oracle on W + B @ A unrounded (>= 40 dB), far from the base model's output. Parity against peft itself is
+    unpinned (peft is not installed); the adapter math is peft's published base(x) + B(A(x)) * alpha / r, r = alpha."""
+    from f_lite.lora import merge_lora_
+    from oracle import flite_ref as R
+
+    m = DiT.random(seed=0, device=DEV, **PRESETS[preset])
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 16, 16, 16, generator=g).bfloat16()
+    ctx = torch.randn(2, 24, 128, generator=g).bfloat16()
+    t = torch.tensor([0.7, 0.7])
+    base = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32).cpu()
+    lsd = {}
+    for name, mod in m.named_modules():
+        if isinstance(mod, torch.nn.Linear) and name.rsplit(".", 1)[-1] in ("qkv", "q", "context_kv", "proj"):
+            lsd[f"{name}.lora_A.weight"] = torch.randn(8, mod.in_features, generator=g) * 0.05
+            lsd[f"{name}.lora_B.weight"] = torch.randn(mod.out_features, 8, generator=g) * 0.05
+    assert merge_lora_(m, lsd, target_modules=["qkv", "q", "context_kv", "proj"], rank=8) == len(lsd) // 2
+    out = m(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32).cpu()
+    params = R.make_state_dict(R.PRESETS[preset].as_dict(), seed=0)
+    for k in list(params):
+        mod = k[: -len(".weight")]
+        if f"{mod}.lora_A.weight" in lsd:
+            params[k] = params[k] + lsd[f"{mod}.lora_B.weight"] @ lsd[f"{mod}.lora_A.weight"]
+    ref = R.RefDiT(R.PRESETS[preset], params, dtype=torch.float32)(x.float(), ctx.float(), None, t)
+    p, p_base = R.psnr(out, ref), R.psnr(base, ref)
+    print(f"{preset} LoRA-merged forward vs fp32 oracle: {p:.2f} dB (base model: {p_base:.2f} dB)")
+    assert p >= 40.0 and p_base < p - 10

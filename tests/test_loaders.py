@@ -104,8 +104,73 @@ def test_pt_checkpoint_errors(tmp_path):
         load_f_lite_pt(tmp_path / "bad.pt", "cpu", width=512, cross_attn_input_size=128, train_bias_and_rms=True)
     with pytest.raises(NotImplementedError):
         load_f_lite_pt(tmp_path / "bad.pt", "cpu", residual_v=True)
-    with pytest.raises(NotImplementedError):
-        load_f_lite_pt(tmp_path / "bad.pt", "cpu", lora_path="x")
+
+
+def _lora_sd(model, targets=("qkv", "q", "context_kv", "proj"), rank=4, seed=1):
+    """A peft-format LoRA state dict (get_peft_model_state_dict keys: "<module>.lora_A.weight" [r, in],
+    "<module>.lora_B.weight" [out, r]) for every Linear whose name ends in one of `targets`."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for name, mod in model.named_modules():
+        if isinstance(mod, torch.nn.Linear) and any(name == t or name.endswith("." + t) for t in targets):
+            sd[f"{name}.lora_A.weight"] = torch.randn(rank, mod.in_features, generator=g) * 0.1
+            sd[f"{name}.lora_B.weight"] = torch.randn(mod.out_features, rank, generator=g) * 0.1
+    return sd
+
+
+@pytest.mark.parametrize("preset", ["tiny", "tiny_v2"])
+def test_lora_merge(preset):
+    """LoRA folded into the weights (f_lite/lora.py; the reference keeps peft modules, pt.py:107-135):
+    W <- bf16(W + B @ A) for exactly the adapted Linears (qkv, cross q, context_kv, both proj), nothing else."""
+    from f_lite.lora import merge_lora_
+
+    m = _filled(DiT if preset == "tiny" else DiTv2, preset).to(torch.bfloat16)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    lsd = _lora_sd(m)
+    mods = {k.rsplit(".lora_", 1)[0] for k in lsd}
+    assert any(k.endswith("self_attn.qkv") for k in mods) and any(k.endswith("cross_attn.q") for k in mods)
+    assert not any(k.endswith(("context_proj", "final_proj", "gate_proj")) for k in mods)
+    assert merge_lora_(m, lsd, target_modules=["qkv", "q", "context_kv", "proj"], rank=4) == len(mods)
+    for k, v in m.state_dict().items():
+        mod = k[: -len(".weight")] if k.endswith(".weight") else None
+        if mod in mods:
+            want = (before[k].float() + lsd[f"{mod}.lora_B.weight"] @ lsd[f"{mod}.lora_A.weight"]).bfloat16()
+            assert torch.equal(v, want), k
+        else:
+            assert torch.equal(v, before[k]), k
+
+
+def test_lora_pt_loader_and_dit_methods(tmp_path):
+    """load_f_lite_pt(lora_path=...) (pt.py:107-135) and DiT.load_lora_weights / save_lora_weights
+    (model.py:487-495) give the same merged weights; wrong rank, untargeted or half-paired adapters raise."""
+    from f_lite.lora import merge_lora_
+    from f_lite.pt import load_f_lite_pt
+
+    m = _filled(DiT, "tiny")
+    torch.save(m.state_dict(), tmp_path / "model.pt")
+    lsd = _lora_sd(m, rank=8)
+    torch.save(lsd, tmp_path / "lora.pt")
+    kw = dict(width=512, cross_attn_input_size=128, train_bias_and_rms=True)
+    pipe = load_f_lite_pt(tmp_path / "model.pt", "cpu", dtype="bfloat16", lora_path=tmp_path / "lora.pt",
+                          lora_rank=8, **kw)
+    ref = m.to(torch.bfloat16)
+    merge_lora_(ref, lsd)
+    got = pipe.dit_model.state_dict()
+    assert all(torch.equal(got[k], v) for k, v in ref.state_dict().items())
+    # the DiT methods: save the loaded adapter, load it into a fresh copy of the base weights
+    pipe.dit_model.save_lora_weights(tmp_path)
+    fresh = load_f_lite_pt(tmp_path / "model.pt", "cpu", dtype="bfloat16", **kw).dit_model
+    fresh.load_lora_weights(tmp_path)
+    assert all(torch.equal(fresh.state_dict()[k], v) for k, v in got.items())
+    with pytest.raises(ValueError):  # lora_rank disagrees with the file (peft would refuse the shapes)
+        load_f_lite_pt(tmp_path / "model.pt", "cpu", lora_path=tmp_path / "lora.pt", lora_rank=4, **kw)
+    with pytest.raises(KeyError):  # an adapter on a module outside lora_target_modules
+        load_f_lite_pt(tmp_path / "model.pt", "cpu", lora_path=tmp_path / "lora.pt", lora_rank=8,
+                       lora_target_modules="qkv", **kw)
+    half = {k: v for k, v in lsd.items() if not k.startswith("blocks.0.self_attn.qkv.lora_B")}
+    assert len(half) == len(lsd) - 1
+    with pytest.raises(KeyError):
+        merge_lora_(fresh, half)
 
 
 def test_generate_signature_matches_reference():
