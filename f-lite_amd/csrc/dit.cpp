@@ -143,6 +143,7 @@ int DitEngine::bind(const std::string& name, const void* ptr, long numel) {
     // the fp8 copies were quantised from the old storage: fp8 mode stays on and the next forward / sample
     // requantises them (into the same buffers) before it runs
     w8_stale_ = true;
+    ctx_stale_ = true;  // the context K/V were projected with the old weights
   }
   bound_[name] = {ptr, numel};
   const bf16_t* p = (const bf16_t*)ptr;
@@ -353,6 +354,7 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
   FLITE_REQUIRE(n <= nctx_max_, "set_context: context longer than prepared");
   for (int i = 0; i < nseq; ++i) FLITE_REQUIRE(cu_host[i + 1] >= cu_host[i], "set_context: bad cu_seqlens");
   FLITE_HIP_CHECK(hipMemcpyAsync(cu_ctx_, cu_host, (nseq + 1) * 4, hipMemcpyHostToDevice, s));
+  ctx_stale_ = false;
   nctx_ = n;
   nseq_ctx_ = nseq;
   ctx_max_len_ = 0;
@@ -713,6 +715,7 @@ int DitEngine::enable_fp8(hipStream_t s, bool on) {
 
 int DitEngine::weights_updated(hipStream_t s) {
   w8_stale_ = true;
+  ctx_stale_ = true;
   return fp8_ ? quantise_fp8(s) : 0;
 }
 
@@ -934,6 +937,8 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
   FLITE_REQUIRE(x_ != nullptr, "forward: call prepare first");
   FLITE_REQUIRE(Bi * dup == B_, "forward: batch does not match the prepared workspace");
   FLITE_REQUIRE(nseq_ctx_ == B_, "forward: set_context must be called for this batch");
+  FLITE_REQUIRE(!ctx_stale_, "forward: weights changed since set_context (its K/V cache is stale): set the context "
+                "again");
   FLITE_REQUIRE(t_row0 >= 0 && t_row0 + (B_ - 1) * t_row_step < nt_, "forward: timestep rows out of range");
   FLITE_REQUIRE(sp_n_ == 1 || (sp_kv_send_ && sp_kv_recv_ && sp_out_send_ && sp_out_recv_),
                 "forward: sequence parallelism needs its exchange buffers (flite_dit_sp_bind_buffers)");
@@ -1209,6 +1214,8 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
   const int dup = use_cfg ? 2 : 1;
   FLITE_REQUIRE(Bi * dup == B_, "sample: batch does not match the prepared workspace");
   FLITE_REQUIRE(!apg || use_cfg, "sample: APG requires classifier-free guidance");
+  FLITE_REQUIRE(!ctx_stale_, "sample: weights changed since set_context (its K/V cache is stale): set the context "
+                "again");
   if (fp8_ && w8_stale_ && quantise_fp8(s)) return 1;  // before any capture: quantise_fp8 synchronises
   // timesteps: one row per step, shared by every sample of the batch (pipeline.py:260,268)
   FLITE_HIP_CHECK(hipMemcpyAsync(tdev_, t_host, n_steps * 4, hipMemcpyHostToDevice, s));

@@ -146,6 +146,7 @@ class DitEngine {
   };
   bool fp8_ = false;
   bool w8_stale_ = true;  // the fp8 copies do not reflect the bound bf16 weights (requantised before the next use)
+  bool ctx_stale_ = false;  // a weight changed after set_context: the cached context K/V are stale
   std::vector<Fp8W> w8_;
   std::vector<void*> w8_allocs_;
   uint8_t *nbuf8_ = nullptr, *nbuf8_s_ = nullptr, *obuf8_ = nullptr, *obuf8_s_ = nullptr;

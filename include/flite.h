@@ -267,7 +267,9 @@ int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable);
 /*
  * The CONTENTS of bound weights changed in place (a load_state_dict copy, a LoRA merge, re-initialisation):
  * every engine-owned copy derived from them is remade -- in fp8 mode the MXFP8 weights are requantised on
- * `stream` now. The bf16 path reads the bound storage directly and needs nothing. No reference counterpart
+ * `stream` now. The bf16 path reads the bound storage directly. The cross-attention K/V cached by
+ * flite_dit_set_context were projected with the old weights: after this call (or a re-bind to new storage)
+ * flite_dit_forward / flite_dit_sample fail until flite_dit_set_context runs again. No reference counterpart
  * (nn.Linear reads its parameters on every call).
  */
 int flite_dit_weights_updated(flite_dit* dit, void* stream);

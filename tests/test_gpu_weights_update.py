@@ -135,3 +135,24 @@ def test_lora_merged_forward_matches_oracle(preset):
     p, p_base = R.psnr(out, ref), R.psnr(base, ref)
     print(f"{preset} LoRA-merged forward vs fp32 oracle: {p:.2f} dB (base model: {p_base:.2f} dB)")
     assert p >= 40.0 and p_base < p - 10
+
+
+def test_engine_refuses_stale_context():
+    """include/flite.h flite_dit_weights_updated: the context K/V cached by set_context were projected with the old
+    weights, so forward fails until the context is set again (the Python wrappers always set it per call)."""
+    from f_lite import _native
+
+    m = DiT.random(seed=0, device=DEV, **PRESETS["tiny"])
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 16, 16, 16, generator=g).to(DEV)
+    ctx = torch.randn(2 * 24, 128, generator=g).bfloat16().to(DEV)
+    m(x, ctx.view(2, 24, 128), None, torch.tensor([0.5, 0.5]).to(DEV))  # binds and prepares the engine
+    eng = m.engine()
+    out = torch.empty(2, 16, 16, 16, device=DEV)
+    eng.set_context(ctx, [0, 24, 48])
+    eng.forward(x, out, 0, 1)
+    eng.weights_updated(DEV)
+    with pytest.raises(_native.FliteError, match="set the context again"):
+        eng.forward(x, out, 0, 1)
+    eng.set_context(ctx, [0, 24, 48])
+    eng.forward(x, out, 0, 1)
