@@ -33,6 +33,24 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
 __device__ __forceinline__ unsigned pack2bf(float lo, float hi) {
   return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
 }
+// Wide epilogue stores of the GEMMs (gemm.hip, gemm_fp8.hip). For one output row, a 16-column group of a wave is
+// held as 4 columns by each of the lanes lr + 16 lk (lk = 0..3), so one store instruction would write 16 rows of
+// 4-column pieces; every tile of a round stores at the same time, with the MFMA pipes idle. Two such groups a
+// (columns [c, c+16)) and b ([c+16, c+32)), one dword per 2 (bf16) or 4 (e4m3) columns, are re-dealt by one
+// v_permlane16_swap per dword (odd 16-lane rows of `a` <-> even rows of `b`) so that lane lk holds the 8
+// consecutive columns c + deal8_col(lk) + 0..7: half the store instructions, each twice as wide. Every lane must
+// be active (the partner lanes lr + 16 lk share the row, so callers mask only the store).
+__device__ __forceinline__ u32x4 deal8(const u32x2& a, const u32x2& b) {
+  const auto x = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto y = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  return u32x4{x[0], y[0], x[1], y[1]};
+}
+__device__ __forceinline__ u32x2 deal8(unsigned a, unsigned b) {
+  const auto x = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+  return u32x2{x[0], x[1]};
+}
+__device__ __forceinline__ int deal8_col(int lk) { return 8 * (lk >> 1) + 16 * (lk & 1); }
+
 // x * sigmoid(x) with v_exp_f32 and v_rcp_f32 (1 ulp) instead of an IEEE division (~10 VALU per element in
 // the SwiGLU GEMM epilogue). Limits: x -> -inf gives -0, x -> +inf gives x.
 __device__ __forceinline__ float silu_f(float x) {

@@ -288,13 +288,9 @@ struct GemmCta {
   //   k1.lo: MFMA(wy, al) || read ah(k1)
   //   wait for tile t+1 (own copies) + all reads of buffer t&1, barrier, DMA tile t+2 into buffer t&1
   //   k1.hi: MFMA(wy, ah) || read wx, al of k0 of tile t+1 (stale, unused data after the last tile)
-  //   hook (persistent schedule only): the previous tile's deferred epilogue stores, one group per k-tile
-  struct NoHook {
-    __device__ __forceinline__ void operator()() const {}
-  };
-  template <int BUF, class Hook = NoHook>
+  template <int BUF>
   __device__ __forceinline__ void ktile(f32x4 (&acc)[8][4], bf16x8 (&wx)[4], bf16x8 (&wy)[4], bf16x8 (&al)[4],
-                                        bf16x8 (&ah)[4], int kt, const Hook& hook = Hook{}) {
+                                        bf16x8 (&ah)[4], int kt) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) ah[i] = rd_a<BUF>(0, 4 + i);
     wy[0] = rd_w<BUF>(1, 0);
@@ -330,11 +326,6 @@ struct GemmCta {
     mfma_half(acc, wy, ah, 4);
     interleave<8, (MI - 4) * 4>();
     if constexpr (!CONV) stage(wave_m == 1 ? kt + 2 : ke, BUF);
-    if constexpr (!std::is_same<Hook, NoHook>::value) {
-      __builtin_amdgcn_sched_barrier(0);
-      hook();
-      __builtin_amdgcn_sched_barrier(0);
-    }
   }
 
   // acc = A[m0.., kb*64 : kend*64] . W[n0.., same]^T  (setup_tile(m0, n0) first). Every k-tile runs the same
@@ -369,88 +360,6 @@ struct GemmCta {
     if (kt < kend) ktile<0>(acc, wx, wy, al, ah, kt);
   }
 
-  // ---- persistent schedule (gemm_bf16_persistent_kernel) ----
-  // DMA of the first two k-tiles of the tile set up by setup_tile (both LDS buffers must be free)
-  __device__ __forceinline__ void prologue(int kend) {
-    ke = kend;
-    stage(0, 0);
-    stage(1, 1);
-  }
-  // k-tiles J, J+1, ... < ND, each followed by hook(integral_constant<J>) (static store index)
-  template <int J, int ND, class H>
-  __device__ __forceinline__ void peel(f32x4 (&acc)[8][4], bf16x8 (&wx)[4], bf16x8 (&wy)[4], bf16x8 (&al)[4],
-                                       bf16x8 (&ah)[4], const H& h) {
-    if constexpr (J < ND) {
-      ktile<0>(acc, wx, wy, al, ah, J, [&] { h(std::integral_constant<int, J>{}); });
-      ktile<1>(acc, wx, wy, al, ah, J + 1, [&] { h(std::integral_constant<int, J + 1>{}); });
-      peel<J + 2, ND>(acc, wx, wy, al, ah, h);
-    }
-  }
-  // acc = the whole k-range [0, kend) after prologue(kend), once this wave has waited for its copies of k-tile 0;
-  // k-tiles 0 .. ND-1 (kend >= ND, ND even) also run hook(j): the previous tile's deferred stores
-  template <int ND, class H>
-  __device__ __forceinline__ void body(f32x4 (&acc)[8][4], int kend, const H& hook) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    __builtin_amdgcn_s_barrier();
-    bf16x8 wx[4], wy[4], al[4], ah[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      wx[i] = rd_w<0>(0, i);
-      al[i] = rd_a<0>(0, i);
-    }
-    peel<0, ND>(acc, wx, wy, al, ah, hook);
-    int kt = ND;
-    for (; kt + 1 < kend; kt += 2) {
-      ktile<0>(acc, wx, wy, al, ah, kt);
-      ktile<1>(acc, wx, wy, al, ah, kt + 1);
-    }
-    if (kt < kend) ktile<0>(acc, wx, wy, al, ah, kt);
-  }
-
-  // Gated-FF output of one tile, packed (deal8) and held in registers so that its stores can run inside the next
-  // tile's k-loop: w[mi] = 8 output columns of row m_base + 16 mi; a lane whose row or columns are outside the
-  // output stores to an out-of-range buffer offset, which the range check drops (one store per k-tile, no branch).
-  struct Deferred {
-    u32x4 w[MI];
-    unsigned off0;   // byte offset of row m_base, columns oc .. oc + 7
-    unsigned valid;  // bit mi: row m_base + 16 mi and the columns are inside the output
-  };
-  __device__ __forceinline__ void gated_defer(const f32x4 (&acc)[8][4], int m0, int n0, Deferred& d) const {
-    const int F = p.N >> 1;
-    const int m_base = m0 + wave_m * WM + lr;
-    const int oc = (n0 >> 1) + wave_n * 32 + deal8_col();
-    d.off0 = (unsigned)(((long)m_base * p.ldo + oc) * 2);
-    d.valid = 0;
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-      u32x2 v[2];
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const f32x4 g = acc[mi][2 * pr];
-        const f32x4 u = acc[mi][2 * pr + 1];
-        if constexpr (EPI == EPI_SWIGLU_BF16) {
-          v[pr].x = pack2bf(silu_f(g[0]) * u[0], silu_f(g[1]) * u[1]);
-          v[pr].y = pack2bf(silu_f(g[2]) * u[2], silu_f(g[3]) * u[3]);
-        } else {
-          v[pr].x = pack2bf(gelu_tanh_f(g[0]) * u[0], gelu_tanh_f(g[1]) * u[1]);
-          v[pr].y = pack2bf(gelu_tanh_f(g[2]) * u[2], gelu_tanh_f(g[3]) * u[3]);
-        }
-      }
-      d.w[mi] = deal8(v[0], v[1]);
-      d.valid |= (m_base + mi * 16 < p.M && oc < F) ? 1u << mi : 0u;
-    }
-  }
-  template <int J>
-  __device__ __forceinline__ void store_deferred(const Deferred& d, const __amdgpu_buffer_rsrc_t& rs) const {
-    if constexpr (J < MI) {
-      const unsigned off = ((d.valid >> J) & 1) ? d.off0 + (unsigned)(J * 16 * p.ldo * 2) : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b128(d.w[J], rs, (int)off, 0, 0);
-    }
-  }
-
   // Gated residual x[m][n] += gate[seg(m)][n] * (acc + bias[n]) (model.py:289,297,301). A read-modify-write of
   // the fp32 residual: the loads of two accumulator rows (8 x + 8 gate, 16 B per lane) are issued together at
   // clamped, always-valid addresses and only the stores are masked, so the tile pays 4 memory round trips
@@ -474,15 +383,13 @@ struct GemmCta {
     f32x4 g2[2][4];
     int seg_lo = 0;
     if constexpr (TWO_SEG) {
-      {
-        seg_lo = min(m_base, p.M - 1) / p.rows_per_seg;
-        const int seg_hi = min(m_base + (MI - 1) * 16, p.M - 1) / p.rows_per_seg;
+      seg_lo = min(m_base, p.M - 1) / p.rows_per_seg;
+      const int seg_hi = min(m_base + (MI - 1) * 16, p.M - 1) / p.rows_per_seg;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const float* grow = p.gate + (long)(s ? seg_hi : seg_lo) * p.gate_seg_stride;
+      for (int s = 0; s < 2; ++s) {
+        const float* grow = p.gate + (long)(s ? seg_hi : seg_lo) * p.gate_seg_stride;
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni) g2[s][ni] = *(const f32x4*)(grow + nc[ni]);
-        }
+        for (int ni = 0; ni < 4; ++ni) g2[s][ni] = *(const f32x4*)(grow + nc[ni]);
       }
     }
 #pragma unroll
@@ -604,19 +511,8 @@ struct GemmCta {
     }
   }
 
-  // Wide bf16 stores. For one output row, the 16-column group g of a wave is held as 4 columns by each of the lanes
-  // lr + 16 lk (lk = 0..3), so one store instruction would write 16 rows x 32 B as 8-B pieces; the epilogue then
-  // runs at the store issue rate with the MFMA pipes idle (every tile of a round ends together). Two groups (a =
-  // columns [c, c+16), b = [c+16, c+32)) packed as bf16 pairs are re-dealt by one v_permlane16_swap per dword
-  // (odd 16-lane rows of `a` <-> even rows of `b`) so that lane lk holds 8 consecutive columns
-  // c + 8 (lk >> 1) + 16 (lk & 1) + 0..7: half the store instructions, each a 16-B piece, 64 B per row.
-  // Needs every lane active (the partner lanes lr + 16 lk share the row, so callers mask only the store).
-  __device__ __forceinline__ static u32x4 deal8(const u32x2& a, const u32x2& b) {
-    const auto x = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
-    const auto y = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
-    return u32x4{x[0], y[0], x[1], y[1]};
-  }
-  __device__ __forceinline__ int deal8_col() const { return 8 * (lk >> 1) + 16 * (lk & 1); }
+  // Wide bf16 stores (common.h deal8): 16-B pieces, 64 B per row and store instruction instead of 8-B pieces
+  __device__ __forceinline__ int deal8_col() const { return ::flite::deal8_col(lk); }
   // 16-B stores are legal when every row start is 16-B aligned
   __device__ __forceinline__ bool wide_ok() const {
     return (p.ldo & 7) == 0 && ((uintptr_t)p.out & 15) == 0;
@@ -782,72 +678,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmParams p) {
     if (p.pf != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the read-ahead has landed
 }
 
-// Persistent gated-FF GEMM (SwiGLU gate/up, T5 GEGLU) for launches of more tiles than one round of the G CUs.
-// Grid = G workgroups (G % 8 == 0, one per CU). XCD x (= blockIdx % 8, the dispatcher's placement) owns the
-// contiguous range of linear tiles that xcd_remap gives it, and its workgroup j runs tiles j, j + G/8, ... of that
-// range: the hardware dispatcher's order for the one-tile-per-workgroup grid when a round's tiles finish together.
-// Same tiles, same k order, same arithmetic: the output is bit-identical to gemm_bf16_kernel.
-// What changes is the end of a tile. In the one-tile grid every tile of a round stores its output at the same time
-// (14.7 MB per round at 1024^2) while the MFMA pipes idle: the stores cost 4 % of the launch (tools/variants.py
-// ablation, profiles/r03o). Here a tile's output is packed into 28 registers (Deferred) and stored one row group
-// per k-tile during the next tile's first k-tiles, when the memory system carries only the operand stream; the next
-// tile's first two k-tiles are staged before the packing, so their DMA lands meanwhile. Only the last tile of a
-// workgroup stores at its end.
-template <int EPI, int MI>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_persistent_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  using Cta = GemmCta<EPI, false, MI>;
-  static_assert(Cta::GATED_FF, "persistent schedule: gated-FF epilogues only");
-  constexpr int ND = (MI + 1) & ~1;  // k-tiles that carry a deferred store (even: the loop is unrolled x2)
-  Cta c(p, smem);
-  const int num_m = (p.M + Cta::BMV - 1) / Cta::BMV;
-  const int num_n = (p.N + BN - 1) / BN;
-  const int nk = p.K / BK;
-  const int T = num_m * num_n;
-  const int x = blockIdx.x & 7, per = (int)gridDim.x >> 3, q = T >> 3, r = T & 7;
-  const int s_x = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-  const int c_x = x < r ? q + 1 : q;
-  int i = (int)blockIdx.x >> 3;
-  if (i >= c_x) return;
-  const __amdgpu_buffer_rsrc_t out_rs =
-      __builtin_amdgcn_make_buffer_rsrc(p.out, (short)0, (int)((long)p.M * p.ldo * 2), 0x00020000);
-  f32x4 acc[8][4];
-  typename Cta::Deferred d;
-  int m0, n0;
-  sk::tile_origin(s_x + i, num_m, num_n, m0, n0, Cta::BMV, BN);
-  c.setup_tile(m0, n0);
-  c.prologue(nk);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  c.template body<0>(acc, nk, [](auto) {});
-  for (;;) {
-    // every wave has finished reading the operand buffers (incl. the last k-tile's look-ahead reads)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const int in = i + per;
-    const bool more = in < c_x;
-    int m1 = 0, n1 = 0;
-    if (more) {
-      sk::tile_origin(s_x + in, num_m, num_n, m1, n1, Cta::BMV, BN);
-      c.setup_tile(m1, n1);
-      c.prologue(nk);
-    }
-    c.gated_defer(acc, m0, n0, d);
-    if (!more) {
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const unsigned off = ((d.valid >> mi) & 1) ? d.off0 + (unsigned)(mi * 16 * p.ldo * 2) : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b128(d.w[mi], out_rs, (int)off, 0, 0);
-      }
-      break;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the next tile's first k-tiles
-    c.template body<ND>(acc, nk, [&](auto jc) { c.template store_deferred<decltype(jc)::value>(d, out_rs); });
-    i = in;
-    m0 = m1;
-    n0 = n1;
-  }
-}
-
 int g_num_cu = 0;
 
 // stream-K split (stream_k.h) when the caller passed a workspace
@@ -869,19 +699,8 @@ bool use_bm224(const GemmParams& p) {
   return r224 < 0.97 * r256;
 }
 
-// Persistent schedule for a gated-FF launch of `tiles` 224-row tiles (gemm_bf16_persistent_kernel; with 256-row
-// tiles the 32 deferred-store registers do not fit beside the accumulators): more than one round,
-// at least 8 k-tiles to carry the deferred stores, 16-B aligned output rows addressable by a buffer descriptor,
-// no read-ahead. FLITE_GEMM_NO_PERSIST=1 turns it off (A/B switch for measurements).
-bool use_persist(const GemmParams& p, int tiles) {
-  static const bool off = getenv("FLITE_GEMM_NO_PERSIST") != nullptr;
-  return !off && g_num_cu > 0 && g_num_cu % 8 == 0 && tiles > g_num_cu && p.K / BK >= 8 && p.pf == nullptr &&
-         (p.ldo & 7) == 0 && ((uintptr_t)p.out & 15) == 0 && (long)p.M * p.ldo * 2 < (1L << 31);
-}
-
 template <int EPI>
 int launch(GemmParams p, hipStream_t s) {
-  constexpr bool GATED = EPI == EPI_SWIGLU_BF16 || EPI == EPI_GEGLU_BF16;
   const int num_n = (p.N + BN - 1) / BN;
   const int T = (p.M + BM - 1) / BM * num_n;
   p.sk_tiles = choose_sk_tiles(p, T, &p.sk_wgs);
@@ -892,12 +711,7 @@ int launch(GemmParams p, hipStream_t s) {
     hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(g_num_cu), dim3(NT), LDS_ALLOC, s, p);
   } else if (use_bm224(p)) {
     const int T224 = (p.M + 223) / 224 * num_n;
-    if (GATED && use_persist(p, T224)) {
-      if constexpr (GATED)
-        hipLaunchKernelGGL((gemm_bf16_persistent_kernel<EPI, 7>), dim3(g_num_cu), dim3(NT), LDS_ALLOC, s, p);
-    } else {
-      hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 7>), dim3(T224), dim3(NT), LDS_ALLOC, s, p);
-    }
+    hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 7>), dim3(T224), dim3(NT), LDS_ALLOC, s, p);
   } else {
     hipLaunchKernelGGL((gemm_bf16_kernel<EPI, false, 8>), dim3(T), dim3(NT), LDS_ALLOC, s, p);
   }
@@ -914,11 +728,6 @@ hipError_t set_attrs() {
   e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, false, 7>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           LDS_ALLOC);
   if (e != hipSuccess) return e;
-  if constexpr (EPI == EPI_SWIGLU_BF16 || EPI == EPI_GEGLU_BF16) {
-    e = hipFuncSetAttribute((const void*)gemm_bf16_persistent_kernel<EPI, 7>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC);
-    if (e != hipSuccess) return e;
-  }
   if constexpr (EPI == EPI_STORE_BF16 || EPI == EPI_STORE_F32)
     return hipFuncSetAttribute((const void*)gemm_bf16_kernel<EPI, true, 8>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC);

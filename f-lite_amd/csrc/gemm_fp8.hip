@@ -348,21 +348,31 @@ struct Fp8Cta {
           for (int r = 0; r < 4; ++r) acc[mi][ni][r] *= rn;
       }
     }
+    const bool wide = wide_ok();  // N % 256 == 0: no column tail
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       const int m = m_base + mi * 16;
-      if (m >= p.M) continue;
+      u32x2 pk[4];
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
-        const int n = n_base + ni * 16;
-        if (n >= p.N) continue;
-        u32x2 w;
-        w.x = pack2bf(acc[mi][ni][0], acc[mi][ni][1]);
-        w.y = pack2bf(acc[mi][ni][2], acc[mi][ni][3]);
-        *(u32x2*)((bf16_t*)p.out + (long)m * p.ldo + n) = w;
+        pk[ni].x = pack2bf(acc[mi][ni][0], acc[mi][ni][1]);
+        pk[ni].y = pack2bf(acc[mi][ni][2], acc[mi][ni][3]);
+      }
+      bf16_t* orow = (bf16_t*)p.out + (long)m * p.ldo;
+      if (wide) {  // common.h deal8: 16-B pieces
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const u32x4 w = deal8(pk[2 * q], pk[2 * q + 1]);
+          if (m < p.M) *(u32x4*)(orow + n_base - lk * 4 + 32 * q + deal8_col(lk)) = w;
+        }
+      } else if (m < p.M) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) *(u32x2*)(orow + n_base + ni * 16) = pk[ni];
       }
     }
   }
+  // 16-B bf16 stores are legal when every row start is 16-B aligned
+  __device__ __forceinline__ bool wide_ok() const { return (p.ldo & 7) == 0 && ((uintptr_t)p.out & 15) == 0; }
 
   // ---- epilogues: lane holds C[m][n..n+3], m = m_base + mi*16, n = n_base + ni*16 (gemm.hip layout) ----
   __device__ __forceinline__ void epilogue(f32x4 (&acc)[8][4], int m0, int n0) {
@@ -375,6 +385,7 @@ struct Fp8Cta {
       if (oc0 >= F) return;
       const int blk = oc0 >> 5;
       uint8_t* o8 = (uint8_t*)p.out;
+      const bool wide = (p.ldo & 7) == 0 && ((uintptr_t)p.out & 7) == 0;
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
         const int m = m_base + mi * 16;
@@ -390,12 +401,16 @@ struct Fp8Cta {
         amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
         const int e = mx_exp(amax);
         const float inv = mx_inv(e);
-        if (m < p.M) {
+        const unsigned lo = pack4_fp8(h, inv), hi = pack4_fp8(h + 4, inv);  // columns 4 lk .. and 16 + 4 lk ..
+        if (wide) {  // common.h deal8: one 8-B piece per row instead of two 4-B pieces
+          const u32x2 w = deal8(lo, hi);
+          if (m < p.M) *(u32x2*)(o8 + (long)m * p.ldo + oc0 + deal8_col(lk)) = w;
+        } else if (m < p.M) {
           uint8_t* orow = o8 + (long)m * p.ldo + oc0 + lk * 4;
-          *(unsigned*)(orow) = pack4_fp8(h, inv);
-          *(unsigned*)(orow + 16) = pack4_fp8(h + 4, inv);
-          if (lk == 0) p.out_sc[((long)(blk >> 2) * p.out_rows_pad + m) * 4 + (blk & 3)] = (uint8_t)(e + 127);
+          *(unsigned*)(orow) = lo;
+          *(unsigned*)(orow + 16) = hi;
         }
+        if (m < p.M && lk == 0) p.out_sc[((long)(blk >> 2) * p.out_rows_pad + m) * 4 + (blk & 3)] = (uint8_t)(e + 127);
       }
       return;
     } else if constexpr (EPI == EPI8_RESID_F32) {
@@ -451,19 +466,29 @@ struct Fp8Cta {
           const int n = n_base + ni * 16 + r;
           bias[ni][r] = (p.bias != nullptr && n < p.N) ? bf2f(p.bias[n]) : 0.f;
         }
+      const bool wide = (p.N & 7) == 0 && wide_ok();  // an 8-column group of deal8 is inside or outside [0, N)
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
         const int m = m_base + mi * 16;
-        if (m >= p.M) continue;
+        u32x2 pk[4];
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
-          const int n = n_base + ni * 16;
-          if (n >= p.N) continue;
           const f32x4 v = acc[mi][ni];
-          u32x2 w;
-          w.x = pack2bf(v[0] + bias[ni][0], v[1] + bias[ni][1]);
-          w.y = pack2bf(v[2] + bias[ni][2], v[3] + bias[ni][3]);
-          *(u32x2*)((bf16_t*)p.out + (long)m * p.ldo + n) = w;
+          pk[ni].x = pack2bf(v[0] + bias[ni][0], v[1] + bias[ni][1]);
+          pk[ni].y = pack2bf(v[2] + bias[ni][2], v[3] + bias[ni][3]);
+        }
+        bf16_t* orow = (bf16_t*)p.out + (long)m * p.ldo;
+        if (wide) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const u32x4 w = deal8(pk[2 * q], pk[2 * q + 1]);
+            const int n = n_base - lk * 4 + 32 * q + deal8_col(lk);
+            if (m < p.M && n < p.N) *(u32x4*)(orow + n) = w;
+          }
+        } else if (m < p.M) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            if (n_base + ni * 16 < p.N) *(u32x2*)(orow + n_base + ni * 16) = pk[ni];
         }
       }
     }

@@ -115,13 +115,12 @@ def test_gemm_224_row_tiles(M):
     assert rel(sw, torch.nn.functional.silu(a.float() @ wg.float().t()) * (a.float() @ wu.float().t())) < 1e-2
 
 
-# Gated-FF GEMMs of more than one round of 224-row tiles run persistent with their output stores deferred into the
-# next tile's k-loop (gemm.hip gemm_bf16_persistent_kernel) when the output rows are 16-B aligned; a misaligned
-# output view takes the one-tile-per-workgroup kernel with 8-B stores. Same tiles and k order: bit-identical.
+# Gated-FF GEMM epilogues store 16-B pieces re-dealt across lanes by v_permlane16_swap (common.h deal8) when the
+# output rows are 16-B aligned; a misaligned output view takes the 8-B-store path. Same values: bit-identical.
 # Ragged M (8174: a last tile of 110 rows) and F % 32 == 16 (the last 16 output columns of a tile masked).
 @pytest.mark.parametrize("M,F", [(8224, 12288), (8174, 3088)])
 @pytest.mark.parametrize("epi", ["swiglu", "geglu"])
-def test_gemm_gated_persistent_bit_identical(M, F, epi):
+def test_gemm_gated_wide_stores_bit_identical(M, F, epi):
     K = 512
     g = torch.Generator(device=DEV).manual_seed(M + F)
     a = torch.randn(M, K, device=DEV, generator=g).bfloat16()
@@ -133,7 +132,7 @@ def test_gemm_gated_persistent_bit_identical(M, F, epi):
     act = torch.nn.functional.silu(gf) if epi == "swiglu" else torch.nn.functional.gelu(gf, approximate="tanh")
     assert rel(out, act * uf) < 1e-2
     buf = torch.full((M, F + 8), -1.0, device=DEV, dtype=torch.bfloat16)
-    view = buf[:, 4:4 + F]  # 8-B aligned rows: the non-persistent kernel
+    view = buf[:, 4:4 + F]  # 8-B aligned rows: the 8-B-store path
     nat.gemm(a, wg, epilogue=e, w2=wu, out=view)
     assert torch.equal(view, out)
     assert bool((buf[:, :4] == -1).all()) and bool((buf[:, 4 + F:] == -1).all())  # nothing stored outside
