@@ -691,12 +691,16 @@ int choose_sk_tiles(const GemmParams& p, int T, int* gs) {
 // G CUs (e.g. M = 8224, N = 3072: 444 tiles = 2 rounds of 7/8-size tiles instead of 396 = 2 full rounds);
 // stream-K (256-row tiles only) keeps priority where its model takes it.
 bool use_bm224(const GemmParams& p) {
-  if (p.conv_in != nullptr || g_num_cu <= 0) return false;
+  static const bool off = getenv("FLITE_GEMM_NO_BM224") != nullptr;  // A/B switch for measurements
+  if (off || p.conv_in != nullptr || g_num_cu <= 0) return false;
   const int G = g_num_cu;
   const int num_n = (p.N + BN - 1) / BN;
   const int t256 = (p.M + 255) / 256 * num_n, t224 = (p.M + 223) / 224 * num_n;
   const double r256 = (double)((t256 + G - 1) / G), r224 = (double)((t224 + G - 1) / G) * 0.875;
-  return r224 < 0.97 * r256;
+  // A 224-row tile streams 7 % more operand bytes per FLOP through L2 and the fabric than a 256-row one. On the
+  // power-limited part that costs clock: inside the sampling loop the gate/up GEMM (predicted 12.25 vs 13 rounds)
+  // ran 2.8 % FASTER with 256-row tiles (profiles/r03q). So 224 rows only where they save a large share of a round.
+  return r224 < 0.93 * r256;
 }
 
 template <int EPI>
