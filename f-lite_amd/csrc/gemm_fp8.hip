@@ -548,13 +548,14 @@ int init8() {
   return 0;
 }
 
-// 224-row tiles where they take fewer rounds x tile size on the chip (gemm.hip use_bm224)
+// 224-row tiles where they take a large share of a round fewer rounds x tile size on the chip (gemm.hip use_bm224:
+// the 256-row tile's fewer operand bytes per FLOP win smaller margins in the power-limited loop)
 bool bm224(const GemmFp8Params& p) {
   if (g_cus <= 0) return false;
   const int num_n = (p.N + BN - 1) / BN;
   const int t256 = (p.M + 255) / 256 * num_n, t224 = (p.M + 223) / 224 * num_n;
   const double r256 = (double)((t256 + g_cus - 1) / g_cus), r224 = (double)((t224 + g_cus - 1) / g_cus) * 0.875;
-  return r224 < 0.97 * r256;
+  return r224 < 0.93 * r256;
 }
 
 template <int EPI>

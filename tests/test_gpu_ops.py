@@ -86,9 +86,10 @@ def test_gemm_gated_residual(shared):
     assert rel(x, ref) < 1e-5
 
 
-# 224-row tiles (gemm.hip use_bm224): on 256 CUs, M = 8224 / 8174 with N = 3072 (and 2F = 24576 for SwiGLU) take
-# 2 (14) rounds of 7/8-size tiles instead of 2 (13) full rounds, so the launcher runs MI = 7. Ragged last tiles
-# (8224 = 36 x 224 + 160, 8174 = 36 x 224 + 110) and every epilogue those GEMMs use.
+# 224-row tiles (gemm.hip use_bm224): on 256 CUs, M = 8224 / 8174 with N = 3072 (also 2F = 3072 for SwiGLU) take
+# 2 rounds of 7/8-size tiles instead of 2 full rounds, so the launcher runs MI = 7; 2F = 24576 (the DiT's gate/up:
+# 14 rounds of 224 rows against 13 of 256) runs 256-row tiles. Ragged last tiles (8224 = 36 x 224 + 160,
+# 8174 = 36 x 224 + 110) and every epilogue those GEMMs use.
 @pytest.mark.parametrize("M", [8224, 8174])
 def test_gemm_224_row_tiles(M):
     N, K, T = 3072, 128, 4112
@@ -108,11 +109,11 @@ def test_gemm_224_row_tiles(M):
     x = x0.clone()
     nat.gemm(a, w, b, out=x, epilogue=nat.EPI_RESID_F32, gate=gate, gate_seg_stride=N, rows_per_seg=T)
     assert rel(x, ref) < 1e-5
-    F = 12288
-    wg = (torch.randn(F, K, device=DEV, generator=g) * 0.05).bfloat16()
-    wu = (torch.randn(F, K, device=DEV, generator=g) * 0.05).bfloat16()
-    sw = nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu)
-    assert rel(sw, torch.nn.functional.silu(a.float() @ wg.float().t()) * (a.float() @ wu.float().t())) < 1e-2
+    for F in (1536, 12288):
+        wg = (torch.randn(F, K, device=DEV, generator=g) * 0.05).bfloat16()
+        wu = (torch.randn(F, K, device=DEV, generator=g) * 0.05).bfloat16()
+        sw = nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu)
+        assert rel(sw, torch.nn.functional.silu(a.float() @ wg.float().t()) * (a.float() @ wu.float().t())) < 1e-2
 
 
 # Gated-FF GEMM epilogues store 16-B pieces re-dealt across lanes by v_permlane16_swap (common.h deal8) when the
