@@ -175,6 +175,10 @@ struct GemmCta {
           a_off[i] = (unsigned)((long)b * p.conv_ih * p.conv_iw * p.conv_c + chunk * 8) * 2u;
         } else {
           a_off[i] = (unsigned)(((long)am * p.lda + chunk * 8) * 2);
+          // 224-row tiles: wave 7's pieces are rows 224-255, which no MFMA reads. An out-of-range offset makes
+          // the copy a zero fill that moves no bytes (7 % fewer operand bytes through L2 and the fabric; on the
+          // power-limited part bytes cost clock, profiles/r03q). Same instruction count, same vmcnt accounting.
+          if (MI == 7 && wave == 7 && (long)p.M * p.lda * 2 <= 0x7fffffffL) a_off[i] = 0x80000000u;
         }
       }
       {

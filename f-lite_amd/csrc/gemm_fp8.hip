@@ -156,6 +156,8 @@ struct Fp8Cta {
         const int chunk = (lane & 7) ^ swz(row);
         const int am = min(m0 + row, p.M - 1);
         a_off[i] = (unsigned)((long)am * p.lda + chunk * 16);
+        // 224-row tiles: rows 224-255 are never read; an out-of-range offset moves no bytes (gemm.hip setup_tile)
+        if (MI == 7 && wave == 7 && (long)p.M * p.lda <= 0x7fffffffL) a_off[i] = 0x80000000u;
       }
       {
         const int row = (wave + 8 * i) * 8 + (lane >> 3);
