@@ -128,6 +128,7 @@ struct GemmCta {
   unsigned a_off[4], w_off[4];
   int cyx[4];  // CONV: output pixel (y << 16 | x) of the piece's row
   int ke;      // end of the k-tile range being staged
+  int tm0;     // first output row of the tile
 
   __device__ __forceinline__ GemmCta(const GemmParams& p_, char* smem) : p(p_) {
     tid = threadIdx.x;
@@ -160,6 +161,7 @@ struct GemmCta {
   // interleave (16-row sub-tiles alternate gate / up) all of a wave's W pieces come from one tensor.
   // Both operands are addressed as buffers: per-lane byte offset of (row, chunk) + uniform k offset in soffset.
   __device__ __forceinline__ void setup_tile(int m0, int n0) {
+    tm0 = m0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       {
@@ -264,27 +266,33 @@ struct GemmCta {
   __device__ __forceinline__ bf16x8 rd_a(int s, int mi) const {
     return *(const LDS_AS bf16x8*)(ab[s] + BUF * TILE_BYTES + mi * 16 * 128);
   }
-  // 16 MFMAs: A rows mi0..mi0+3 x all 4 W fragments
+  // 16 MFMAs: A rows mi0..mi0+3 x all 4 W fragments (MV: the wave's 16-row blocks that hold output rows)
+  template <int MV>
   __device__ __forceinline__ static void mfma_half(f32x4 (&acc)[8][4], const bf16x8 (&wf)[4],
                                                    const bf16x8 (&af)[4], int mi0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
-        if (mi0 + i < MI)
+        if (mi0 + i < MV)
           acc[mi0 + i][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], af[i], acc[mi0 + i][ni], 0, 0, 0);
   }
   // spread NR ds_reads over a half-step's NM MFMAs
   template <int NR, int NM = 16>
   __device__ __forceinline__ static void interleave() {
-    constexpr int per = NM / NR;
+    if constexpr (NM > 0) {
+      constexpr int per = NM / NR;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      __builtin_amdgcn_sched_group_barrier(SG_MFMA, per, 0);
-      __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
+      for (int i = 0; i < NR; ++i) {
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, per, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, NM - per * NR, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(SG_MFMA, NM - per * NR, 0);
   }
+  // MFMAs in the low (mi 0..3) and high (mi 4..7) half-steps of a wave with MV live row blocks
+  static constexpr int lo_mfmas(int mv) { return (mv < 4 ? mv : 4) * 4; }
+  static constexpr int hi_mfmas(int mv) { return (mv > 4 ? mv - 4 : 0) * 4; }
 
   // One 64-deep k-tile from LDS buffer BUF. Register sets: wx / wy = W fragments of alternating k-steps,
   // al / ah = A fragments mi 0..3 / 4..7.
@@ -292,25 +300,25 @@ struct GemmCta {
   //   k1.lo: MFMA(wy, al) || read ah(k1)
   //   wait for tile t+1 (own copies) + all reads of buffer t&1, barrier, DMA tile t+2 into buffer t&1
   //   k1.hi: MFMA(wy, ah) || read wx, al of k0 of tile t+1 (stale, unused data after the last tile)
-  template <int BUF>
+  template <int BUF, int MV>
   __device__ __forceinline__ void ktile(f32x4 (&acc)[8][4], bf16x8 (&wx)[4], bf16x8 (&wy)[4], bf16x8 (&al)[4],
                                         bf16x8 (&ah)[4], int kt) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) ah[i] = rd_a<BUF>(0, 4 + i);
     wy[0] = rd_w<BUF>(1, 0);
     wy[1] = rd_w<BUF>(1, 1);
-    mfma_half(acc, wx, al, 0);
-    interleave<6>();
+    mfma_half<MV>(acc, wx, al, 0);
+    interleave<6, lo_mfmas(MV)>();
     wy[2] = rd_w<BUF>(1, 2);
     wy[3] = rd_w<BUF>(1, 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) al[i] = rd_a<BUF>(1, i);
-    mfma_half(acc, wx, ah, 4);
-    interleave<6, (MI - 4) * 4>();
+    mfma_half<MV>(acc, wx, ah, 4);
+    interleave<6, hi_mfmas(MV)>();
 #pragma unroll
     for (int i = 0; i < 4; ++i) ah[i] = rd_a<BUF>(1, 4 + i);
-    mfma_half(acc, wy, al, 0);
-    interleave<4>();
+    mfma_half<MV>(acc, wy, al, 0);
+    interleave<4, lo_mfmas(MV)>();
     // Round-1 ablation builds priced this wait on MI355X: 3.5 % of the gate/up GEMM and 8-11 % of the K = 12288
     // projections (operands streamed from HBM), nothing at K = 3072, N <= 9216.
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -327,8 +335,8 @@ struct GemmCta {
       wx[i] = rd_w<BUF ^ 1>(0, i);
       al[i] = rd_a<BUF ^ 1>(0, i);
     }
-    mfma_half(acc, wy, ah, 4);
-    interleave<8, (MI - 4) * 4>();
+    mfma_half<MV>(acc, wy, ah, 4);
+    interleave<8, hi_mfmas(MV)>();
     if constexpr (!CONV) stage(wave_m == 1 ? kt + 2 : ke, BUF);
   }
 
@@ -350,6 +358,23 @@ struct GemmCta {
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    // Ragged last tile: a wave whose 16-row blocks lie (partly) past row M skips their MFMAs. At M = 8224 with
+    // 256-row tiles the last of 33 M-tiles holds 32 rows, so 2.7 % of the gate/up, qkv and down MFMA work was
+    // spent on rows that are never stored (energy on a power-limited part, profiles/r03q). Staging, barriers and
+    // fragment reads are those of the full loop, so every wave of the workgroup still meets every barrier.
+    const int live = p.M - (tm0 + wave_m * WM);  // uniform per wave
+    const int mv = live <= 0 ? 0 : min((live + 15) >> 4, MI);
+    if (mv > 4)
+      kloop<MI>(acc, kb, kend);
+    else if (mv > 2)
+      kloop<(MI < 4 ? MI : 4)>(acc, kb, kend);
+    else if (mv > 0)
+      kloop<2>(acc, kb, kend);
+    else
+      kloop<0>(acc, kb, kend);
+  }
+  template <int MV>
+  __device__ __forceinline__ void kloop(f32x4 (&acc)[8][4], int kb, int kend) {
     bf16x8 wx[4], wy[4], al[4], ah[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -358,10 +383,10 @@ struct GemmCta {
     }
     int kt = kb;
     for (; kt + 1 < kend; kt += 2) {
-      ktile<0>(acc, wx, wy, al, ah, kt);
-      ktile<1>(acc, wx, wy, al, ah, kt + 1);
+      ktile<0, MV>(acc, wx, wy, al, ah, kt);
+      ktile<1, MV>(acc, wx, wy, al, ah, kt + 1);
     }
-    if (kt < kend) ktile<0>(acc, wx, wy, al, ah, kt);
+    if (kt < kend) ktile<0, MV>(acc, wx, wy, al, ah, kt);
   }
 
   // Gated residual x[m][n] += gate[seg(m)][n] * (acc + bias[n]) (model.py:289,297,301). A read-modify-write of
