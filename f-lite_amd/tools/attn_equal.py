@@ -43,9 +43,12 @@ def compare(a, b):
     A, B = torch.load(a, weights_only=True), torch.load(b, weights_only=True)
     bad = 0
     for i, (x, y) in enumerate(zip(A, B)):
-        eq = torch.equal(x, y)
-        diff = (x.float() - y.float()).abs().max().item()
-        print(f"case {i} {CASES[i][:3]}: {'identical' if eq else 'DIFFERENT'} (max abs diff {diff:.3e})", flush=True)
+        # bit patterns, so NaNs in the same places compare equal
+        eq = torch.equal(x.view(torch.int16), y.view(torch.int16))
+        diff = (x.float() - y.float()).abs().nan_to_num(0.0).max().item()
+        nans = (int(x.float().isnan().sum()), int(y.float().isnan().sum()))
+        print(f"case {i} {CASES[i][:3]}: {'identical' if eq else 'DIFFERENT'} (max abs diff {diff:.3e}, NaNs {nans})",
+              flush=True)
         bad += not eq
     sys.exit(1 if bad else 0)
 
