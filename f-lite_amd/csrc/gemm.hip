@@ -178,7 +178,7 @@ struct GemmCta {
         } else {
           a_off[i] = (unsigned)(((long)am * p.lda + chunk * 8) * 2);
           // 224-row tiles: wave 7's pieces are rows 224-255, which no MFMA reads. An out-of-range offset makes
-          // the copy a zero fill that moves no bytes (7 % fewer operand bytes through L2 and the fabric; on the
+          // the copy a zero fill that moves no bytes (1/8 of the A stream through L2 and into LDS; on the
           // power-limited part bytes cost clock, profiles/r03q). Same instruction count, same vmcnt accounting.
           if (MI == 7 && wave == 7 && (long)p.M * p.lda * 2 <= 0x7fffffffL) a_off[i] = 0x80000000u;
         }
@@ -726,9 +726,11 @@ bool use_bm224(const GemmParams& p) {
   const int num_n = (p.N + BN - 1) / BN;
   const int t256 = (p.M + 255) / 256 * num_n, t224 = (p.M + 223) / 224 * num_n;
   const double r256 = (double)((t256 + G - 1) / G), r224 = (double)((t224 + G - 1) / G) * 0.875;
-  // A 224-row tile streams 7 % more operand bytes per FLOP through L2 and the fabric than a 256-row one. On the
-  // power-limited part that costs clock: inside the sampling loop the gate/up GEMM (predicted 12.25 vs 13 rounds)
-  // ran 2.8 % FASTER with 256-row tiles (profiles/r03q). So 224 rows only where they save a large share of a round.
+  // A 224-row tile issues 14 % more LDS-DMA pieces (it stages 256 A rows; since round 3 the unread ones move no
+  // bytes) and reads 4.5 % more LDS bytes per FLOP than a 256-row one. On the power-limited part that costs clock:
+  // inside the sampling loop the gate/up GEMM (predicted 12.25 vs 13 rounds) ran 2.8 % FASTER with 256-row tiles
+  // (profiles/r03q; its L2-fabric bytes per launch did not change, 2.36 GB). So 224 rows only where they save a
+  // large share of a round.
   return r224 < 0.93 * r256;
 }
 

@@ -551,7 +551,7 @@ int init8() {
 }
 
 // 224-row tiles where they take a large share of a round fewer rounds x tile size on the chip (gemm.hip use_bm224:
-// the 256-row tile's fewer operand bytes per FLOP win smaller margins in the power-limited loop)
+// the 256-row tile's fewer LDS-DMA pieces and LDS bytes per FLOP win smaller margins in the power-limited loop)
 bool bm224(const GemmFp8Params& p) {
   if (g_cus <= 0) return false;
   const int num_n = (p.N + BN - 1) / BN;

@@ -26,6 +26,7 @@ if not torch.cuda.is_available():  # pragma: no cover
 
 import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
+from _mp import pack, unpack  # noqa: E402
 
 from f_lite import APGConfig, DiT, FLitePipeline  # noqa: E402
 from f_lite import _native  # noqa: E402
@@ -63,19 +64,19 @@ def _worker(rank, port, q):
         apg = APGConfig(enabled=True)
         m = DiT.random(seed=0, device="cuda", **PRESETS["tiny"])
         lat, pos, neg = _inputs(2)
-        q.put(("cfg", rank, cfg_parallel_sample(m, lat.cuda(), pos.cuda(), neg.cuda(), STEPS, G, apg=apg).cpu()))
+        q.put(pack(("cfg", rank, cfg_parallel_sample(m, lat.cuda(), pos.cuda(), neg.cuda(), STEPS, G, apg=apg).cpu())))
         lat3, pos3, neg3 = _inputs(3)
-        q.put(("dp", rank, data_parallel_sample(m, lat3.cuda(), pos3.cuda(), neg3.cuda(), STEPS, G,
-                                                apg=apg).cpu()))
+        q.put(pack(("dp", rank, data_parallel_sample(m, lat3.cuda(), pos3.cuda(), neg3.cuda(), STEPS, G,
+                                                     apg=apg).cpu())))
         # the pipeline surface of the data-parallel mode
         pipe = FLitePipeline(m)
         pipe.enable_data_parallel()
         out = pipe(prompt_embeds=pos3.cuda(), negative_prompt_embeds=neg3.cuda(), latents=lat3.cuda(), height=128,
                    width=128, num_inference_steps=STEPS, guidance_scale=G, apg_config=apg,
                    output_type="latent").images
-        q.put(("dp_pipe", rank, out.float().cpu()))
-        q.put(("sp", rank, sequence_parallel_sample(m, lat.cuda(), pos.cuda(), neg.cuda(), STEPS, G,
-                                                    apg=apg).cpu()))
+        q.put(pack(("dp_pipe", rank, out.float().cpu())))
+        q.put(pack(("sp", rank, sequence_parallel_sample(m, lat.cuda(), pos.cuda(), neg.cuda(), STEPS, G,
+                                                         apg=apg).cpu())))
         torch.cuda.synchronize()
         dist.destroy_process_group()
     except Exception as e:  # report instead of leaving the parent waiting
@@ -94,7 +95,7 @@ def results():
         p.start()
     res = {}
     while len(res) < 8:
-        kind, rank, v = q.get(timeout=110)
+        kind, rank, v = unpack(q.get(timeout=110))
         if kind == "error":
             for p in procs:
                 p.kill()

@@ -18,6 +18,7 @@ if not torch.cuda.is_available():  # pragma: no cover
 
 import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
+from _mp import pack, unpack  # noqa: E402
 
 from f_lite import DiT, FLitePipeline  # noqa: E402
 from f_lite import _native  # noqa: E402
@@ -69,10 +70,10 @@ def _worker(rank, port, q):
         explicit = cfg_parallel_sample(m, lat0.cuda(), pos.cuda(), neg.cuda(), num_inference_steps=STEPS,
                                        guidance_scale=G)
         torch.cuda.synchronize()
-        q.put((rank, acc.cpu()))
-        q.put((rank + 2, via_pipe.cpu()))
-        q.put((rank + 4, own.cpu()))
-        q.put((rank + 6, explicit.cpu()))
+        q.put(pack((rank, acc.cpu())))
+        q.put(pack((rank + 2, via_pipe.cpu())))
+        q.put(pack((rank + 4, own.cpu())))
+        q.put(pack((rank + 6, explicit.cpu())))
         dist.destroy_process_group()
     except Exception as e:  # report instead of leaving the parent waiting
         q.put((rank, repr(e)))
@@ -88,7 +89,7 @@ def two_rank_result():
         p.start()
     res = {}
     while len(res) < 8 and not any(isinstance(v, str) for v in res.values()):
-        k, v = q.get(timeout=100)
+        k, v = unpack(q.get(timeout=100))
         res[k] = v
     for p in procs:
         p.join(30)

@@ -17,6 +17,7 @@ if not torch.cuda.is_available():  # pragma: no cover
 
 import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
+from _mp import pack, unpack  # noqa: E402
 
 from f_lite import DiT, FLitePipeline  # noqa: E402
 from f_lite import _native  # noqa: E402
@@ -68,7 +69,7 @@ def _worker(rank, port, q):
         ctx = broadcast_context(_ctx(rank), src=0)
         out = {i: _image(pipe, ctx, i) for i in image_indices(N_IMAGES, rank, WORLD)}
         torch.cuda.synchronize()
-        q.put((rank, out))
+        q.put(pack((rank, out)))
         dist.destroy_process_group()
     except Exception as e:  # report instead of leaving the parent waiting
         q.put((rank, repr(e)))
@@ -84,7 +85,7 @@ def ranks():
         p.start()
     res = {}
     while len(res) < WORLD and not any(isinstance(v, str) for v in res.values()):
-        k, v = q.get(timeout=100)
+        k, v = unpack(q.get(timeout=100))
         res[k] = v
     for p in procs:
         p.join(30)
