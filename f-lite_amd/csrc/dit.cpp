@@ -30,6 +30,13 @@ bool w_prefetch() {
   return on;
 }
 
+// Block 0 of a CFG batch runs its self-attention sub-block once per image instead of once per CFG copy (forward);
+// FLITE_NO_CFG_DEDUP=1 runs it on every copy (A/B switch for measurements)
+bool cfg_dedup() {
+  static const bool on = getenv("FLITE_NO_CFG_DEDUP") == nullptr;
+  return on;
+}
+
 // the norm2 pass reading the cross-q weights ahead (NormModParams::pf); FLITE_NO_NORM_PF=1 turns only it off
 bool norm_prefetch() {
   static const bool on = w_prefetch() && getenv("FLITE_NO_NORM_PF") == nullptr;
@@ -488,8 +495,13 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   const float *shift_mlp = mod + 6L * D, *scale_mlp = mod + 7L * D, *gate_mlp = mod + 8L * D;
 
   // pf0/pf1: weights of the GEMM that reads this norm's output, read ahead into the Infinity Cache (w_prefetch)
+  // sa_seqs_ > 0 (forward, block 0 of a CFG batch): the self-attention sub-block runs on the first sa_seqs_
+  // sequences only, and its residual rows are then copied to the other CFG copies (they are identical until the
+  // cross-attention, which sees each copy's own context)
+  const int Bsa = sa_seqs_ > 0 ? sa_seqs_ : B_;
+  const long Msa = (long)Bsa * Tl_;
   auto norm = [&](const bf16_t* w, const float* sh, const float* sc, const bf16_t* pf0 = nullptr, long pf0_n = 0,
-                  const bf16_t* pf1 = nullptr, long pf1_n = 0) -> int {
+                  const bf16_t* pf1 = nullptr, long pf1_n = 0, long rows = 0) -> int {
     NormModParams nm;
     if (norm_prefetch()) {
       nm.pf[0] = pf0;
@@ -505,14 +517,14 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     nm.shift = sh;
     nm.scale = sc;
     nm.mod_seg_stride = mseg;
-    nm.rows = M_;
+    nm.rows = rows > 0 ? rows : M_;
     nm.D = D;
     nm.in_seg = Tl_;
     nm.in_stride = Tl_;
     nm.in_off = 0;
     return rmsnorm_mod(nm, false, s);
   };
-  auto resid = [&](const bf16_t* A, long lda, const bf16_t* W, int K, const float* gate) -> int {
+  auto resid = [&](const bf16_t* A, long lda, const bf16_t* W, int K, const float* gate, long rows = 0) -> int {
     GemmParams g;
     g.A = A;
     g.lda = lda;
@@ -523,7 +535,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.gate = gate;
     g.gate_seg_stride = mseg;
     g.rows_per_seg = Tl_;
-    g.M = (int)M_;
+    g.M = (int)(rows > 0 ? rows : M_);
     g.N = D;
     g.K = K;
     return gemm(g, EPI_RESID_F32, s);
@@ -531,7 +543,8 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   const long rope_off = (long)sp_rank_ * Tl_ * 128;  // table rows of the tokens held here
 
   // --- self attention ---
-  if (norm(b.norm1, shift_sa, scale_sa)) return 1;
+  const bool probe_sa = Msa == M_;  // the kernel probes average full-batch launches only
+  if (norm(b.norm1, shift_sa, scale_sa, nullptr, 0, nullptr, 0, Msa)) return 1;
   {
     GemmParams g;
     g.A = nbuf_;
@@ -545,22 +558,22 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
       g.pf = b.proj_w;
       g.pf_bytes = (long)D * D * 2;
     }
-    g.M = (int)M_;
+    g.M = (int)Msa;
     g.N = 3 * D;
     g.K = D;
     // RoPE + QK-norm of the q and k heads ("(k h d)" layout, model.py:163) in the GEMM epilogue
     g.rope = rope_axes();
     g.norm_cols = 2 * D;
     g.rope_cols = cfg.use_rope ? 2 * D : 0;
-    if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
+    if (probe_sa && probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
     if (gemm(g, fuse_qk_norm() ? EPI_QKV_NORM_BF16 : EPI_STORE_BF16, s)) return 1;
-    if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
+    if (probe_sa && probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
   }
   if (!fuse_qk_norm()) {
     RopeNormParams rn;
     rn.x = qkv_;
     rn.ldx = 3L * D;
-    rn.rows = M_;
+    rn.rows = Msa;
     rn.heads = 2 * H;  // q heads then k heads ("(k h d)" layout, model.py:163)
     rn.rope_heads = cfg.use_rope ? 2 * H : 0;
     rn.cos = cos_ + rope_off;
@@ -584,7 +597,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = HEAD_DIM;
     a.cu_q = cu_self_;
     a.cu_k = sp_n_ > 1 ? cu_full_ : cu_self_;
-    a.B = B_;
+    a.B = Bsa;
     a.H = H;
     a.head_dim = HEAD_DIM;
     a.max_q = Tl_;
@@ -593,11 +606,13 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.max_score = kQKNormScoreBound;
     a.split_ws = attn_ws_;
     a.split_ws_bytes = attn_ws_bytes_;
-    if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
+    if (probe_sa && probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
     if (sp_rng ? sp_ring_attention(s, a) : sp_ovl ? sp_self_attention(s, a) : attn_fwd(a, s)) return 1;
-    if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
+    if (probe_sa && probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
   }
-  if (resid(obuf_, D, b.proj_w, D, gate_sa)) return 1;
+  if (resid(obuf_, D, b.proj_w, D, gate_sa, Msa)) return 1;
+  for (long r0 = Msa; r0 < M_; r0 += Msa)  // the other CFG copies of the residual rows
+    FLITE_HIP_CHECK(hipMemcpyAsync(x_ + r0 * D, x_, (size_t)Msa * D * sizeof(float), hipMemcpyDeviceToDevice, s));
 
   // --- cross attention (model.py:291-297) ---
   if (b.cross) {
@@ -994,7 +1009,13 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     char name[32];
     snprintf(name, sizeof(name), "flite.block.%d", i);
     RoctxRange range(name);
-    if (fp8_ ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg)) return 1;
+    // CFG batch (dup copies of each latent, one timestep row): the copies' residual streams agree until block 0's
+    // cross-attention, so its self-attention sub-block runs once per image (1/dup of the 40-block self-attention
+    // work of block 0; bf16 path, one rank)
+    sa_seqs_ = (i == 0 && dup > 1 && t_row_step == 0 && sp_n_ == 1 && !fp8_ && cfg_dedup()) ? Bi : 0;
+    const int rc = fp8_ ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg);
+    sa_seqs_ = 0;
+    if (rc) return 1;
   }
   // final stage (model.py:575-581): drop registers, RMSNorm (fp32 weight multiply), modulate, project
   {

@@ -115,6 +115,7 @@ class DitEngine {
   hipEvent_t ev_ring_[2] = {nullptr, nullptr}, ev_used_[2] = {nullptr, nullptr};
   bool attn_mx_ = true;  // fp8 path: the attention writes the proj GEMM's MXFP8 operand itself
   long M_ = 0;
+  int sa_seqs_ = 0;  // > 0: block 0's self-attention on the first sa_seqs_ sequences only (forward, CFG batch)
   int nctx_ = 0, nseq_ctx_ = 0, ctx_max_len_ = 0;
   // workspace
   float* x_ = nullptr;
