@@ -779,7 +779,10 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   const float *shift_sa = mod, *scale_sa = mod + D, *gate_sa = mod + 2L * D;
   const float *shift_ca = mod + 3L * D, *scale_ca = mod + 4L * D, *gate_ca = mod + 5L * D;
   const float *shift_mlp = mod + 6L * D, *scale_mlp = mod + 7L * D, *gate_mlp = mod + 8L * D;
-  auto norm8 = [&](const bf16_t* w, const float* sh, const float* sc) -> int {
+  const int Bsa = sa_seqs_ > 0 ? sa_seqs_ : B_;  // as run_block: block 0 of a CFG batch, self-attention once
+  const long Msa = (long)Bsa * Tl_;
+  const bool probe_sa = Msa == M_;
+  auto norm8 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0) -> int {
     NormModParams nm;
     nm.x = x_;
     nm.ldx = D;
@@ -791,7 +794,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     nm.shift = sh;
     nm.scale = sc;
     nm.mod_seg_stride = mseg;
-    nm.rows = M_;
+    nm.rows = rows > 0 ? rows : M_;
     nm.D = D;
     nm.in_seg = Tl_;
     nm.in_stride = Tl_;
@@ -800,7 +803,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   };
   auto g8 = [&](const uint8_t* A, const uint8_t* As, const uint8_t* W, const uint8_t* Ws, long w_rows, int N, int K,
                 const bf16_t* bias, int epi, void* out, long ldo, const float* gate, int norm_cols = 0,
-                int rope_cols = 0) -> int {
+                int rope_cols = 0, long rows = 0) -> int {
     GemmFp8Params g;
     g.A = A;
     g.lda = K;
@@ -816,7 +819,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     g.gate = gate;
     g.gate_seg_stride = mseg;
     g.rows_per_seg = Tl_;
-    g.M = (int)M_;
+    g.M = (int)(rows > 0 ? rows : M_);
     g.N = N;
     g.K = K;
     if (epi == EPI8_SWIGLU_FP8) {
@@ -834,7 +837,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     return gemm_fp8(g, epi, s);
   };
   auto attn = [&](const bf16_t* qp, long ldq, const bf16_t* kp, const bf16_t* vp, long ldkv, const int* cu_k,
-                  int max_k) -> int {
+                  int max_k, int nseq = 0) -> int {
     AttnParams a;
     a.q = qp;
     a.k = kp;
@@ -846,7 +849,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = HEAD_DIM;
     a.cu_q = cu_self_;
     a.cu_k = cu_k;
-    a.B = B_;
+    a.B = nseq > 0 ? nseq : B_;
     a.H = H;
     a.head_dim = HEAD_DIM;
     a.max_q = Tl_;
@@ -862,11 +865,11 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     }
     return attn_fwd(a, s);
   };
-  auto qk_norm = [&](long ldx, int heads, int rope_heads) -> int {
+  auto qk_norm = [&](long ldx, int heads, int rope_heads, long rows = 0) -> int {
     RopeNormParams rn;
     rn.x = qkv_;
     rn.ldx = ldx;
-    rn.rows = M_;
+    rn.rows = rows > 0 ? rows : M_;
     rn.heads = heads;
     rn.rope_heads = rope_heads;
     if (rope_heads > 0) {
@@ -877,19 +880,21 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     return rope_qknorm(rn, s);
   };
   // --- self attention ---
-  if (norm8(b.norm1, shift_sa, scale_sa)) return 1;
-  if (probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
+  if (norm8(b.norm1, shift_sa, scale_sa, Msa)) return 1;
+  if (probe_sa && probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
   const bool fused = fuse_qk_norm();  // RoPE + QK-norm in the GEMM epilogue (the weights were quantised to match)
   if (g8(nbuf8_, nbuf8_s_, q.qkv, q.qkv_s, 3L * D, 3 * D, D, b.qkv_b, fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16,
-         qkv_, 3L * D, nullptr, 2 * D, cfg.use_rope ? 2 * D : 0))
+         qkv_, 3L * D, nullptr, 2 * D, cfg.use_rope ? 2 * D : 0, Msa))
     return 1;
-  if (probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
-  if (!fused && qk_norm(3L * D, 2 * H, cfg.use_rope ? 2 * H : 0)) return 1;
-  if (probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
-  if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, Tl_)) return 1;
-  if (probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
-  if (!attn_mx_ && quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
-  if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa)) return 1;
+  if (probe_sa && probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
+  if (!fused && qk_norm(3L * D, 2 * H, cfg.use_rope ? 2 * H : 0, Msa)) return 1;
+  if (probe_sa && probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
+  if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, Tl_, Bsa)) return 1;
+  if (probe_sa && probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
+  if (!attn_mx_ && quant_rows_fp8(obuf_, D, Msa, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
+  if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa, 0, 0, Msa)) return 1;
+  for (long r0 = Msa; r0 < M_; r0 += Msa)  // the other CFG copies of the residual rows
+    FLITE_HIP_CHECK(hipMemcpyAsync(x_ + r0 * D, x_, (size_t)Msa * D * sizeof(float), hipMemcpyDeviceToDevice, s));
   // --- cross attention ---
   if (b.cross) {
     if (norm8(b.norm2, shift_ca, scale_ca)) return 1;
@@ -1010,9 +1015,9 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     snprintf(name, sizeof(name), "flite.block.%d", i);
     RoctxRange range(name);
     // CFG batch (dup copies of each latent, one timestep row): the copies' residual streams agree until block 0's
-    // cross-attention, so its self-attention sub-block runs once per image (1/dup of the 40-block self-attention
-    // work of block 0; bf16 path, one rank)
-    sa_seqs_ = (i == 0 && dup > 1 && t_row_step == 0 && sp_n_ == 1 && !fp8_ && cfg_dedup()) ? Bi : 0;
+    // cross-attention, so block 0's self-attention sub-block runs once per image instead of once per copy (one
+    // rank; bf16 and MXFP8 paths)
+    sa_seqs_ = (i == 0 && dup > 1 && t_row_step == 0 && sp_n_ == 1 && cfg_dedup()) ? Bi : 0;
     const int rc = fp8_ ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg);
     sa_seqs_ = 0;
     if (rc) return 1;
