@@ -175,14 +175,22 @@ def test_gemm_stream_k(M, N, K):
     assert rel(out, ref) < 1e-2
 
 
-def test_gemm_stream_k_swiglu():
-    M, F, K = 2000, 1152, 8192  # N = 2F = 2304: 72 tiles, stream-K
+@pytest.mark.parametrize("M,F,K", [(2000, 1152, 8192),    # N = 2F = 2304: 72 tiles, stream-K by the model
+                                   (8224, 12288, 3072)])  # the DiT gate/up: 12 rounds + 96 leftover tiles
+def test_gemm_stream_k_swiglu(M, F, K):
     a = torch.randn(M, K, device=DEV).bfloat16()
     wg = (torch.randn(F, K, device=DEV) * 0.05).bfloat16()
     wu = (torch.randn(F, K, device=DEV) * 0.05).bfloat16()
     ref = torch.nn.functional.silu(a.float() @ wg.float().t()) * (a.float() @ wu.float().t())
-    out = nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu, workspace=nat.gemm_workspace(DEV))
+    ws = nat.gemm_workspace(DEV)
+    out = nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu, workspace=ws)
     assert rel(out, ref) < 1e-2
+    dp = nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu)
+    assert rel(dp, ref) < 1e-2
+    assert not torch.equal(out, dp)  # the split path ran (different fp32 summation order in the leftover tiles)
+    assert torch.equal(out, nat.gemm(a, wg, epilogue=nat.EPI_SWIGLU_BF16, w2=wu, workspace=ws))  # deterministic
+    n_cu = ws.numel() // (256 * 256 * 4 + 4)
+    assert int(ws[n_cu * 256 * 256 * 4:].view(torch.int32).abs().sum().item()) == 0  # every flag back to 0
 
 
 def _attn_ref(q, k, v, cu_q, cu_k, scale):
