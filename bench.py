@@ -75,17 +75,54 @@ def host_info():
         info["numa_nodes"] = len([p for p in Path("/sys/devices/system/node").glob("node[0-9]*")])
     except OSError:
         pass
+    info.update(cgroup_cpu_quota())
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
     return info
 
 
-def cpu_threads() -> int:
-    """torch threads for the CPU baseline: every core this process may run on (sched affinity), capped by
-    OMP_NUM_THREADS when the host sets it (the GPU box grants each job a 16-core share of a larger machine)."""
-    n = host_info()["affinity_cores"]
+def cgroup_cpu_quota() -> dict:
+    """The CPU bandwidth quota of this process's cgroup: v2 `cpu.max` ("<quota> <period>" or "max <period>") or
+    v1 `cpu.cfs_quota_us` / `cpu.cfs_period_us`. Returns the raw text and the granted CPUs (None when unlimited)."""
+    out = {"cgroup_cpu_max": None, "cgroup_cpus": None}
+    try:
+        rel = ""
+        for line in Path("/proc/self/cgroup").read_text().splitlines():
+            if line.startswith("0::"):
+                rel = line[3:].strip()
+        for f in (Path("/sys/fs/cgroup") / rel.lstrip("/") / "cpu.max", Path("/sys/fs/cgroup/cpu.max")):
+            if f.exists():
+                raw = f.read_text().strip()
+                out["cgroup_cpu_max"] = f"{f}: {raw}"
+                q, per = raw.split()[:2]
+                if q != "max":
+                    out["cgroup_cpus"] = int(q) / int(per)
+                return out
+        q = Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us")
+        if q.exists():
+            quota = int(q.read_text())
+            per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+            out["cgroup_cpu_max"] = f"cgroup v1 cfs_quota_us {quota} cfs_period_us {per}"
+            if quota > 0:
+                out["cgroup_cpus"] = quota / per
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def cpu_threads() -> "tuple[int, str]":
+    """torch threads for the CPU baseline and why: every CPU the cgroup quota grants (capped by the affinity set);
+    without a quota, every core of the affinity set capped by OMP_NUM_THREADS when the host sets it (the GPU box
+    asks each job to keep to a 16-CPU share of a larger machine)."""
+    info = host_info()
+    n = info["affinity_cores"]
+    if info.get("cgroup_cpus"):
+        q = max(1, int(info["cgroup_cpus"]))
+        return max(1, min(n, q)), f"cgroup quota grants {info['cgroup_cpus']:g} CPUs ({info['cgroup_cpu_max']})"
     omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        n = min(n, int(omp))
-    return max(1, n)
+    if omp and omp.isdigit() and int(omp) > 0 and int(omp) < n:
+        return int(omp), (f"no cgroup CPU quota ({info['cgroup_cpu_max']}); OMP_NUM_THREADS={omp} of "
+                          f"{n} affinity cores (the box's per-job CPU share)")
+    return max(1, n), f"no cgroup CPU quota ({info['cgroup_cpu_max']}); all {n} affinity cores"
 
 
 def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blocks: int = 3):
@@ -103,7 +140,7 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
     from oracle import flite_ref as R
     from oracle import vae_ref as VR
 
-    threads = cpu_threads()
+    threads, why = cpu_threads()
     prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     D = cfg["hidden_size"]
@@ -157,6 +194,7 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
         "value": 1.0 / per_image,
         "unit": "images/s",
         "cores": threads,
+        "cores_reason": why,
         "kind": "port",
         "extrapolated": True,
         "sample": (f"fp32 CPU port (oracle/flite_ref.py, oracle/vae_ref.py) at {H}x{W}, CFG batch 2 (T={T}): "
@@ -177,7 +215,7 @@ def cpu_baseline_full(model, vae, cfg: dict, H: int, W: int, steps: int, k_steps
     from oracle import flite_ref as R
     from oracle import vae_ref as VR
 
-    threads = cpu_threads()
+    threads, why = cpu_threads()
     prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     rcfg = R.DiTConfig(**{k: cfg[k] for k in ("in_channels", "patch_size", "hidden_size", "depth", "num_heads",
@@ -214,7 +252,8 @@ def cpu_baseline_full(model, vae, cfg: dict, H: int, W: int, steps: int, k_steps
     torch.set_num_threads(prev_threads)
     per_image = res["dit_steps_s"] * steps / k_steps + res["vae_s"]
     return {
-        "value": 1.0 / per_image, "unit": "images/s", "cores": threads, "kind": "port", "extrapolated": True,
+        "value": 1.0 / per_image, "unit": "images/s", "cores": threads, "cores_reason": why, "kind": "port",
+        "extrapolated": True,
         "sample": (f"fp32 CPU port (oracle/flite_ref.py sample loop + oracle/vae_ref.py) at {H}x{W}: {k_steps} whole "
                    f"CFG-6 steps of the {steps}-step schedule {res['dit_steps_s']:.1f} s, VAE decode "
                    f"{res['vae_s']:.1f} s; per image = {steps}/{k_steps} x {res['dit_steps_s']:.1f} + "
@@ -260,7 +299,14 @@ def main():
                     help="images per bench step and GPU, sampled as ONE batch (num_images_per_prompt; M = 2 x B x T)")
     ap.add_argument("--fp8", action="store_true",
                     help="BASELINE configs[4]: block GEMMs on MXFP8 weights + activations (block-scaled fp8 MFMA)")
+    ap.add_argument("--fp8-bf16-blocks", default="",
+                    help="with --fp8: comma-separated block indices that keep bf16 GEMMs (precision policy)")
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
+    ap.add_argument("--mode", default="replica", choices=["replica", "cfg-parallel", "sp", "sp-ring"],
+                    help="replica: image i on GPU i mod N (the metric line); cfg-parallel: the two CFG branches of an "
+                         "image on a pair of GPUs; sp / sp-ring: one image over all N GPUs, token rows split, K/V "
+                         "all-gathered per block (sp) or shifted round a ring (sp-ring). The latency modes are "
+                         "single-image lines (SURVEY §8f rank 1), not the metric")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -273,6 +319,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU is required")
+    if args.mode == "cfg-parallel" and world % 2:
+        raise SystemExit("--mode cfg-parallel pairs the ranks: --gpus must be even")
+    if args.mode in ("sp", "sp-ring") and world < 2:
+        raise SystemExit(f"--mode {args.mode} splits one image over the ranks: --gpus must be >= 2")
+    if args.mode != "replica" and (args.images_per_gpu != 1 or args.guidance < 1.0):
+        raise SystemExit("the latency modes run one CFG image per group (--images-per-gpu 1, --guidance >= 1)")
     # FLITE_BENCH_REHEARSAL=1: rehearse the N-rank path on a box with fewer GPUs (ranks share GPUs round-robin,
     # gloo instead of RCCL, which refuses two ranks on one device). Never the measured configuration: the line
     # says so in "distributed".
@@ -299,8 +351,9 @@ def main():
 
     cfg = dict(PRESETS[args.model])
     model = DiT.random(seed=0, device=dev, **cfg)
+    keep16 = [int(b) for b in args.fp8_bf16_blocks.split(",") if b.strip()]
     if args.fp8:
-        model.enable_fp8(True)
+        model.enable_fp8(True, bf16_blocks=keep16)
     vae = None
     if not args.no_vae:
         from f_lite.vae import AutoencoderKL
@@ -319,6 +372,18 @@ def main():
     lh, lw = args.height // 8, args.width // 8
 
     BI = args.images_per_gpu
+    # work units: replica = one rank; cfg-parallel = a pair of ranks (uncond, cond); sp = all ranks
+    if args.mode == "cfg-parallel":
+        pairs = [dist.new_group([2 * i, 2 * i + 1]) for i in range(world // 2)]  # every rank creates every group
+        pipe.enable_cfg_parallel(pairs[rank // 2])
+        n_units, unit = world // 2, rank // 2
+    elif args.mode in ("sp", "sp-ring"):
+        pipe.enable_sequence_parallel(None, ring=args.mode == "sp-ring")
+        n_units, unit = 1, 0
+    else:
+        n_units, unit = world, rank
+    if args.mode != "replica":
+        args.probe = "none"  # the per-launch probe shapes assume whole CFG batches on one GPU
 
     def latents_for(i):  # step i of this rank: images i * BI .. i * BI + BI - 1
         lats = []
@@ -334,7 +399,7 @@ def main():
                     num_inference_steps=args.sample_steps, guidance_scale=args.guidance, output_type=out_type,
                     num_images_per_prompt=BI, use_graph=not args.no_graph).images
 
-    mine = image_indices(world * (args.steps + args.warmup), rank, world)  # image i -> GPU i mod N
+    mine = image_indices(n_units * (args.steps + args.warmup), unit, n_units)  # image i -> unit i mod n_units
     for w in range(args.warmup):
         one_image(mine[args.steps + w])
     kinds = {"gateup": nat.PROBE_GEMM_GATEUP, "attn": nat.PROBE_ATTN_SELF, "down": nat.PROBE_GEMM_DOWN,
@@ -358,7 +423,7 @@ def main():
     probe_ms = []
     if args.probe != "none":
         eng.set_probe(kinds[args.probe], 4 * cfg["depth"] * args.sample_steps)
-        pipe(prompt_embeds=ctx, latents=latents_for(rank), height=args.height, width=args.width,
+        pipe(prompt_embeds=ctx, latents=latents_for(unit), height=args.height, width=args.width,
              num_inference_steps=args.sample_steps, guidance_scale=args.guidance, output_type=out_type,
              num_images_per_prompt=BI, use_graph=False)
         torch.cuda.synchronize()
@@ -370,13 +435,19 @@ def main():
         return
 
     ms_per_step = elapsed / args.steps * 1000.0
-    value = world * args.steps * BI / elapsed
+    value = n_units * args.steps * BI / elapsed
     f_step, f_once = dit_flops(cfg, args.height, args.width, args.sample_steps)
     f_vae = vae_flops(args.height, args.width) if vae is not None else 0.0
-    f_image = args.sample_steps * 2 * f_step + 2 * f_once + f_vae
     D = cfg["hidden_size"]
     F = int(D * cfg["mlp_ratio"])
     T = 16 + (args.height // 16) * (args.width // 16)
+    # the reference's work per image, and what this path skips: in the replica mode the two CFG copies of an image
+    # share block 0's self-attention sub-block (qkv GEMM, attention, proj GEMM: identical inputs until block 0's
+    # cross-attention, dit.cpp forward), computed once per step instead of twice
+    f_ref_image = args.sample_steps * 2 * f_step + 2 * f_once + f_vae
+    dedup = args.mode == "replica" and args.guidance >= 1.0 and os.environ.get("FLITE_NO_CFG_DEDUP") is None
+    f_dedup = args.sample_steps * (2 * T * D * 3 * D + 4 * T * T * D + 2 * T * D * D) if dedup else 0.0
+    f_image = f_ref_image - f_dedup
     M = 2 * BI * T
     per_launch = {
         "gateup": (2.0 * M * 2 * F * D, "SwiGLU gate/up GEMM (M=%d, N=%d, K=%d)" % (M, 2 * F, D)),
@@ -423,6 +494,8 @@ def main():
                                                             args.model.upper(), "fp8" if args.fp8 else "bf16")
     if (args.model, args.height, args.width, args.sample_steps, args.fp8) == ("10b", 1024, 1024, 30, False):
         metric += "; 1/8 GPU + MFMA util%"  # BASELINE.json's metric string (util in mfma_util_image)
+    if args.mode != "replica":
+        metric += " [single-image latency mode: %s]" % args.mode
     line = {
         "metric": metric,
         "value": round(value, 5),
@@ -432,7 +505,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 2),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.mode in ("sp", "sp-ring") else "weak",
         "vs_baseline": None,
         "dtype": ("fp8 (MXFP8: OCP e4m3 weights+activations, E8M0 scale per 32; block GEMMs) + bf16 attention"
                   if args.fp8 else "bf16"),
@@ -442,17 +515,30 @@ def main():
             args.model.upper(), "model_v2 layout" if cfg["per_block_adaln"] else "model.py layout",
             args.width, args.height, args.sample_steps, args.guidance,
             "VAE decode to uint8" if vae is not None else "latents only (no VAE)"),
-                   "images_per_gpu_per_step": BI, "cfg_batch": 2, "parallelism": "replica dp%d" % world,
-                   "hipgraph": not args.no_graph, "vae_tiling": bool(args.vae_tiling)},
+                   "images_per_gpu_per_step": BI, "cfg_batch": 2,
+                   "parallelism": {"replica": "replica dp%d" % world, "cfg-parallel": "cfg-parallel %d pair(s)" % n_units,
+                                   "sp": "sequence parallel sp%d (K/V all-gather per block)" % world,
+                                   "sp-ring": "sequence parallel sp%d (ring K/V shifts)" % world}[args.mode],
+                   "hipgraph": not args.no_graph, "vae_tiling": bool(args.vae_tiling),
+                   "fp8_bf16_blocks": keep16 if args.fp8 else None},
         "distributed": {"world_size": world,
                         "backend": ("gloo REHEARSAL (ranks share %d GPU(s); not a measurement)"
                                     % torch.cuda.device_count() if rehearsal else
                                     "nccl (RCCL over xGMI)" if world > 1 else "none"),
-                        "collectives": "one broadcast of the [1,512,4096] context from rank 0 before the loop",
-                        "images_per_rank": args.steps},
+                        "collectives": {
+                            "replica": "one broadcast of the [1,512,4096] context from rank 0 before the loop",
+                            "cfg-parallel": "context broadcast + per step one all-gather of the two fp32 branch outputs",
+                            "sp": "context broadcast + per block an all-gather of the K/V rows, per step the output rows",
+                            "sp-ring": "context broadcast + per block N-1 ring shifts of K/V rows, per step the output "
+                                       "rows"}[args.mode],
+                        "images_per_unit": args.steps, "units": n_units},
+        "mode": args.mode,
+        "latency_ms_per_image": round(elapsed / args.steps * 1000.0 / BI, 2),
         "mfma_util_image": round(f_image * value / world / PEAK_BF16, 4),
         "mfma_util_image_peak": "bf16 dense (2.5166 PF) for both dtypes" if args.fp8 else "bf16 dense",
         "algorithmic_flops_per_image": f_image,
+        "reference_flops_per_image": f_ref_image,
+        "cfg_dedup_flops_per_image": f_dedup,
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

@@ -300,6 +300,19 @@ int flite_apg_euler(void* stream, const float* uncond, const float* cond, float*
   return apg_update_nchw(uncond, cond, acc, n, guidance, k, orth_scale, dt, (hipStream_t)stream);
 }
 
+int flite_apg_sums_dev(void* stream, const float* uncond, const float* cond, long n, int phase, float* ws4) {
+  FLITE_REQUIRE(uncond && cond && ws4, "flite_apg_sums_dev: null argument");
+  FLITE_REQUIRE(n >= 0, "flite_apg_sums_dev: negative element count");
+  return apg_sums_dev(uncond, cond, n, phase, ws4, (hipStream_t)stream);
+}
+
+int flite_apg_euler_dev(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
+                        float threshold, long n_total, const float* ws4, float dt) {
+  FLITE_REQUIRE(uncond && cond && acc && ws4, "flite_apg_euler_dev: null argument");
+  FLITE_REQUIRE(n >= 0 && n_total >= n, "flite_apg_euler_dev: bad element counts");
+  return apg_update_nchw_dev(uncond, cond, acc, n, guidance, threshold, n_total, ws4, dt, (hipStream_t)stream);
+}
+
 int flite_dit_forward(flite_dit* dit, void* stream, const void* x, int x_is_bf16, int batch, int t_row0,
                       int t_row_step, void* out, int out_is_bf16) {
   FLITE_REQUIRE(dit && x && out, "flite_dit_forward: null argument");
@@ -464,6 +477,11 @@ int flite_rmsnorm_modulate_fp8(void* stream, const float* x, long ldx, void* y8,
 int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable) {
   FLITE_REQUIRE(dit, "flite_dit_enable_fp8: null engine");
   return dit->eng->enable_fp8((hipStream_t)stream, enable != 0);
+}
+
+int flite_dit_set_fp8_bf16_blocks(flite_dit* dit, const int* blocks, int n) {
+  FLITE_REQUIRE(dit, "flite_dit_set_fp8_bf16_blocks: null engine");
+  return dit->eng->set_fp8_bf16_blocks(blocks, n);
 }
 
 int flite_dit_weights_updated(flite_dit* dit, void* stream) {

@@ -360,13 +360,17 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
   const int n = cu_host[nseq];
   FLITE_REQUIRE(n <= nctx_max_, "set_context: context longer than prepared");
   for (int i = 0; i < nseq; ++i) FLITE_REQUIRE(cu_host[i + 1] >= cu_host[i], "set_context: bad cu_seqlens");
+  // stale until the last K/V projection below has been issued: a failure part-way leaves the cache refused
+  ctx_stale_ = true;
   FLITE_HIP_CHECK(hipMemcpyAsync(cu_ctx_, cu_host, (nseq + 1) * 4, hipMemcpyHostToDevice, s));
-  ctx_stale_ = false;
   nctx_ = n;
   nseq_ctx_ = nseq;
   ctx_max_len_ = 0;
   for (int i = 0; i < nseq; ++i) ctx_max_len_ = std::max(ctx_max_len_, cu_host[i + 1] - cu_host[i]);
-  if (n == 0) return 0;
+  if (n == 0) {
+    ctx_stale_ = false;
+    return 0;
+  }
   // context_proj (model.py:527) -> LigerRMSNorm (model.py:528)
   GemmParams g;
   g.A = (const bf16_t*)ctx;
@@ -413,6 +417,7 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
     rn.rope_heads = 0;
     if (rope_qknorm(rn, s)) return 1;
   }
+  ctx_stale_ = false;
   return 0;
 }
 
@@ -728,6 +733,18 @@ int DitEngine::enable_fp8(hipStream_t s, bool on) {
   return alloc_fp8_act();
 }
 
+int DitEngine::set_fp8_bf16_blocks(const int* blocks, int n) {
+  FLITE_REQUIRE(n >= 0 && (n == 0 || blocks != nullptr), "set_fp8_bf16_blocks: bad block list");
+  std::vector<char> keep(cfg.depth, 0);
+  for (int i = 0; i < n; ++i) {
+    FLITE_REQUIRE(blocks[i] >= 0 && blocks[i] < cfg.depth, "set_fp8_bf16_blocks: block index out of range");
+    keep[blocks[i]] = 1;
+  }
+  drop_graph();  // a cached graph holds the old per-block choice
+  fp8_bf16_blk_.swap(keep);
+  return 0;
+}
+
 int DitEngine::weights_updated(hipStream_t s) {
   w8_stale_ = true;
   ctx_stale_ = true;
@@ -957,8 +974,8 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
   FLITE_REQUIRE(x_ != nullptr, "forward: call prepare first");
   FLITE_REQUIRE(Bi * dup == B_, "forward: batch does not match the prepared workspace");
   FLITE_REQUIRE(nseq_ctx_ == B_, "forward: set_context must be called for this batch");
-  FLITE_REQUIRE(!ctx_stale_, "forward: weights changed since set_context (its K/V cache is stale): set the context "
-                "again");
+  FLITE_REQUIRE(!ctx_stale_, "forward: context K/V cache is stale (weights changed since set_context, or it "
+                "failed): set the context again");
   FLITE_REQUIRE(t_row0 >= 0 && t_row0 + (B_ - 1) * t_row_step < nt_, "forward: timestep rows out of range");
   FLITE_REQUIRE(sp_n_ == 1 || (sp_kv_send_ && sp_kv_recv_ && sp_out_send_ && sp_out_recv_),
                 "forward: sequence parallelism needs its exchange buffers (flite_dit_sp_bind_buffers)");
@@ -1018,7 +1035,8 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     // cross-attention, so block 0's self-attention sub-block runs once per image instead of once per copy (one
     // rank; bf16 and MXFP8 paths)
     sa_seqs_ = (i == 0 && dup > 1 && t_row_step == 0 && sp_n_ == 1 && cfg_dedup()) ? Bi : 0;
-    const int rc = fp8_ ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg);
+    const bool blk8 = fp8_ && !(i < (int)fp8_bf16_blk_.size() && fp8_bf16_blk_[i]);
+    const int rc = blk8 ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg);
     sa_seqs_ = 0;
     if (rc) return 1;
   }
@@ -1240,8 +1258,8 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
   const int dup = use_cfg ? 2 : 1;
   FLITE_REQUIRE(Bi * dup == B_, "sample: batch does not match the prepared workspace");
   FLITE_REQUIRE(!apg || use_cfg, "sample: APG requires classifier-free guidance");
-  FLITE_REQUIRE(!ctx_stale_, "sample: weights changed since set_context (its K/V cache is stale): set the context "
-                "again");
+  FLITE_REQUIRE(!ctx_stale_, "sample: context K/V cache is stale (weights changed since set_context, or it "
+                "failed): set the context again");
   if (fp8_ && w8_stale_ && quantise_fp8(s)) return 1;  // before any capture: quantise_fp8 synchronises
   // timesteps: one row per step, shared by every sample of the batch (pipeline.py:260,268)
   FLITE_HIP_CHECK(hipMemcpyAsync(tdev_, t_host, n_steps * 4, hipMemcpyHostToDevice, s));

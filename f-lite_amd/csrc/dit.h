@@ -50,6 +50,7 @@ class DitEngine {
 
   // fp8 mode (flite_dit_enable_fp8): MXFP8 copies of the block GEMM weights + fp8 activations
   int enable_fp8(hipStream_t s, bool on);
+  int set_fp8_bf16_blocks(const int* blocks, int n);
   // the bound weights' CONTENTS changed in place (flite_dit_weights_updated): requantise the fp8 copies
   int weights_updated(hipStream_t s);
 
@@ -146,6 +147,7 @@ class DitEngine {
     uint8_t *cproj = nullptr, *cproj_s = nullptr, *gu = nullptr, *gu_s = nullptr, *down = nullptr, *down_s = nullptr;
   };
   bool fp8_ = false;
+  std::vector<char> fp8_bf16_blk_;  // blocks that stay bf16 in fp8 mode (flite_dit_set_fp8_bf16_blocks)
   bool w8_stale_ = true;  // the fp8 copies do not reflect the bound bf16 weights (requantised before the next use)
   bool ctx_stale_ = false;  // a weight changed after set_context: the cached context K/V are stale
   std::vector<Fp8W> w8_;

@@ -429,9 +429,22 @@ __global__ __launch_bounds__(1024) void apg_euler_kernel(const float* out, float
 // the whole batch gets bit-identical sums.
 //   phase 0: out = [sum c (c - u), sum c^2]            (dy = c, dd = c - u: pipeline.py:278-281)
 //   phase 1: out = [sum o, sum o^2], o = (c - u) - k c  (orthogonal part, for its std: pipeline.py:282-284)
+// Device-resident scalars (flite_apg_sums_dev / flite_apg_euler_dev): ws[0..1] = the phase-0 sums, ws[2..3] = the
+// phase-1 sums, each after any all-reduce between the ranks; k and the orthogonal scale are derived where they are
+// used, with apg_euler_kernel's fp32 expressions, so a multi-rank APG step needs no host round trip.
+__device__ __forceinline__ float apg_k_of(const float* ws) { return ws[1] > 0.f ? ws[0] / ws[1] : 0.f; }
+__device__ __forceinline__ float apg_scale_of(const float* ws, long n, float thr) {
+  const float so = ws[2], soo = ws[3];
+  const float mean = so / (float)n;
+  const float var = n > 1 ? fmaxf(soo - mean * so, 0.f) / (float)(n - 1) : 0.f;
+  const float sd = sqrtf(var);
+  return sd > 0.f ? fminf(1.f, thr / sd) : 1.f;
+}
+
 __global__ __launch_bounds__(1024) void apg_sums_kernel(const float* u, const float* c, long n, float k, int phase,
-                                                        float* out) {
+                                                        const float* ws_k, float* out) {
   __shared__ float red[32];
+  if (ws_k != nullptr) k = apg_k_of(ws_k);
   float a = 0.f, b = 0.f;
   for (long idx = threadIdx.x; idx < n; idx += blockDim.x) {
     const float uu = u[idx], cc = c[idx];
@@ -452,9 +465,14 @@ __global__ __launch_bounds__(1024) void apg_sums_kernel(const float* u, const fl
   }
 }
 
-// acc += dt * (dy + (g - 1) * sc * orth)   (pipeline.py:285-286,296)
+// acc += dt * (dy + (g - 1) * sc * orth)   (pipeline.py:285-286,296); with ws, k and sc come from the device sums
 __global__ __launch_bounds__(256) void apg_update_nchw_kernel(const float* u, const float* c, float* acc, long n,
-                                                              float g, float k, float sc, float dt) {
+                                                              float g, float k, float sc, float dt, const float* ws,
+                                                              long n_total, float thr) {
+  if (ws != nullptr) {
+    k = apg_k_of(ws);
+    sc = apg_scale_of(ws, n_total, thr);
+  }
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
     const float uu = u[idx], cc = c[idx];
     const float o = (cc - uu) - k * cc;
@@ -681,7 +699,15 @@ int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, 
 
 int apg_sums(const float* u, const float* c, long n, float k, int phase, float* out2, hipStream_t s) {
   FLITE_REQUIRE(phase == 0 || phase == 1, "apg_sums: phase must be 0 or 1");
-  hipLaunchKernelGGL(apg_sums_kernel, dim3(1), dim3(1024), 0, s, u, c, n, k, phase, out2);
+  hipLaunchKernelGGL(apg_sums_kernel, dim3(1), dim3(1024), 0, s, u, c, n, k, phase, (const float*)nullptr, out2);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int apg_sums_dev(const float* u, const float* c, long n, int phase, float* ws4, hipStream_t s) {
+  FLITE_REQUIRE(phase == 0 || phase == 1, "apg_sums_dev: phase must be 0 or 1");
+  hipLaunchKernelGGL(apg_sums_kernel, dim3(1), dim3(1024), 0, s, u, c, n, 0.f, phase,
+                     phase == 1 ? (const float*)ws4 : (const float*)nullptr, ws4 + 2 * phase);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -689,7 +715,17 @@ int apg_sums(const float* u, const float* c, long n, float k, int phase, float* 
 int apg_update_nchw(const float* u, const float* c, float* acc, long n, float g, float k, float sc, float dt,
                     hipStream_t s) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(apg_update_nchw_kernel, dim3(grid_for(n)), dim3(256), 0, s, u, c, acc, n, g, k, sc, dt);
+  hipLaunchKernelGGL(apg_update_nchw_kernel, dim3(grid_for(n)), dim3(256), 0, s, u, c, acc, n, g, k, sc, dt,
+                     (const float*)nullptr, 0L, 0.f);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int apg_update_nchw_dev(const float* u, const float* c, float* acc, long n, float g, float thr, long n_total,
+                        const float* ws4, float dt, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(apg_update_nchw_kernel, dim3(grid_for(n)), dim3(256), 0, s, u, c, acc, n, g, 0.f, 1.f, dt, ws4,
+                     n_total, thr);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

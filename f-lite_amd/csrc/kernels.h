@@ -158,6 +158,9 @@ int unpatchify(const float* out, void* y, bool out_bf16, int B, int C, int H, in
 int apg_sums(const float* u, const float* c, long n, float k, int phase, float* out2, hipStream_t s);
 int apg_update_nchw(const float* u, const float* c, float* acc, long n, float g, float k, float sc, float dt,
                     hipStream_t s);
+int apg_sums_dev(const float* u, const float* c, long n, int phase, float* ws4, hipStream_t s);
+int apg_update_nchw_dev(const float* u, const float* c, float* acc, long n, float g, float thr, long n_total,
+                        const float* ws4, float dt, hipStream_t s);
 int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, float g, float thr, float dt,
               hipStream_t s);
 int timestep_embed(const float* t, bf16_t* emb, int n, int D, int quantize, hipStream_t s);

@@ -79,6 +79,8 @@ SIGNATURES = {
     "flite_dit_sample": (_i, [_vp, _vp, _vp, _i, _i, ctypes.POINTER(_f), ctypes.POINTER(_f), _f, _i, _i, _f, _i]),
     "flite_cfg_euler": (_i, [_vp, _vp, _vp, _vp, _l, _f, _f, _i]),
     "flite_apg_sums": (_i, [_vp, _vp, _vp, _l, _f, _i, _vp]),
+    "flite_apg_sums_dev": (_i, [_vp, _vp, _vp, _l, _i, _vp]),
+    "flite_apg_euler_dev": (_i, [_vp, _vp, _vp, _vp, _l, _f, _f, _l, _vp, _f]),
     "flite_apg_euler": (_i, [_vp, _vp, _vp, _vp, _l, _f, _f, _f, _f]),
     "flite_conv3x3_pack_weight":(_i, [_vp, _vp, _vp, _i, _i, _i]),
     "flite_conv3x3_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i]),
@@ -99,6 +101,7 @@ SIGNATURES = {
                                _l, _i, _vp]),
     "flite_rmsnorm_modulate_fp8": (_i, [_vp, _vp, _l, _vp, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_dit_enable_fp8": (_i, [_vp, _vp, _i]),
+    "flite_dit_set_fp8_bf16_blocks": (_i, [_vp, _vp, _i]),
     "flite_dit_weights_updated": (_i, [_vp, _vp]),
     "flite_vae_weights_updated": (_i, [_vp]),
     "flite_dit_set_sequence_parallel": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -344,6 +347,32 @@ def apg_euler_(acc, uncond, cond, guidance, k, orth_scale, dt):
     return acc
 
 
+def apg_sums_dev(uncond, cond, phase, ws):
+    """flite_apg_sums_dev: phase 0 -> ws[0:2] = [sum c (c - u), sum c^2]; phase 1 (k from ws[0:2], on the device) ->
+    ws[2:4] = [sum o, sum o^2]. `ws` is a 4-float device tensor; nothing returns to the host."""
+    require_gpu(uncond, "uncond", torch.float32)
+    require_gpu(cond, "cond", torch.float32)
+    require_gpu(ws, "ws", torch.float32)
+    if uncond.shape != cond.shape or ws.numel() < 4:
+        raise FliteError("apg_sums_dev: uncond / cond shapes differ, or ws has fewer than 4 floats")
+    check(load().flite_apg_sums_dev(stream_ptr(cond.device), uncond.data_ptr(), cond.data_ptr(), cond.numel(),
+                                    int(phase), ws.data_ptr()), "flite_apg_sums_dev")
+    return ws
+
+
+def apg_euler_dev_(acc, uncond, cond, guidance, threshold, n_total, ws, dt):
+    """flite_apg_euler_dev: the APG + Euler update with k and the orthogonal scale derived from ws on the device."""
+    for t, n in ((acc, "acc"), (uncond, "uncond"), (cond, "cond")):
+        require_gpu(t, n, torch.float32)
+        if t.shape != acc.shape:
+            raise FliteError(f"apg_euler_dev: {n} {tuple(t.shape)} does not match acc {tuple(acc.shape)}")
+    require_gpu(ws, "ws", torch.float32)
+    check(load().flite_apg_euler_dev(stream_ptr(acc.device), uncond.data_ptr(), cond.data_ptr(), acc.data_ptr(),
+                                     acc.numel(), float(guidance), float(threshold), int(n_total), ws.data_ptr(),
+                                     float(dt)), "flite_apg_euler_dev")
+    return acc
+
+
 # ------------------------------------------------------------------------------------------------
 # MXFP8 (include/flite.h: e4m3 elements, one E8M0 scale per 32 K elements, scales [K/128][rows_pad][4])
 # ------------------------------------------------------------------------------------------------
@@ -545,6 +574,12 @@ class DitEngine:
 
     def enable_fp8(self, on: bool = True, device=None):
         check(self.lib.flite_dit_enable_fp8(self.h, stream_ptr(device), int(bool(on))), "flite_dit_enable_fp8")
+
+    def set_fp8_bf16_blocks(self, blocks=()):
+        """Blocks that keep bf16 GEMMs while fp8 mode is on (include/flite.h flite_dit_set_fp8_bf16_blocks)."""
+        blocks = [int(b) for b in blocks]
+        arr = (ctypes.c_int * max(len(blocks), 1))(*blocks)
+        check(self.lib.flite_dit_set_fp8_bf16_blocks(self.h, arr, len(blocks)), "flite_dit_set_fp8_bf16_blocks")
 
     def weights_updated(self, device=None):
         """The bound weights changed in place: remake the engine's derived copies (fp8: requantise)."""

@@ -129,11 +129,26 @@ def apg_step(acc, u, c, dt: float, guidance: float, threshold: float, n_total: i
     return acc
 
 
-def _native_apg_ops():
+def apg_step_device(acc, u, c, dt: float, guidance: float, threshold: float, n_total: int, ws: torch.Tensor,
+                    reduce: Optional[Callable] = None):
+    """apg_step with the scalars kept on the device (include/flite.h flite_apg_sums_dev / flite_apg_euler_dev):
+    the two partial sums of each phase land in the 4-float device tensor `ws`, are optionally all-reduced IN PLACE
+    (RCCL on the device tensor: stream-ordered, no host round trip), and the kernels derive k and the orthogonal
+    scale from them with the fp32 expressions of the single-launch APG kernel. A rank without images (u empty)
+    joins the reductions with zeros."""
     from . import _native
 
-    return (lambda u, c, k, ph: _native.apg_sums(u, c, k, ph),
-            lambda acc, u, c, g, k, sc, dt: _native.apg_euler_(acc, u, c, g, k, sc, dt))
+    have = u.numel() > 0
+    for phase in (0, 1):
+        if have:
+            _native.apg_sums_dev(u, c, phase, ws)
+        else:
+            ws[2 * phase: 2 * phase + 2].zero_()
+        if reduce is not None:
+            reduce(ws[2 * phase: 2 * phase + 2])
+    if have:
+        _native.apg_euler_dev_(acc, u, c, guidance, threshold, n_total, ws, dt)
+    return acc
 
 
 def _broadcast_inputs(group, *ts):
@@ -192,10 +207,10 @@ def cfg_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Tensor,
         return eng.forward(x, out, i, 0)
 
     if apg is not None and apg.enabled:
-        sums, upd = _native_apg_ops()
+        ws = torch.zeros(4, device=dev, dtype=torch.float32)
 
         def update(x, u, c, dt):
-            apg_step(x, u, c, dt, guidance_scale, apg.orthogonal_threshold, x.numel(), sums, upd)
+            apg_step_device(x, u, c, dt, guidance_scale, apg.orthogonal_threshold, x.numel(), ws)
     else:
         def update(x, u, c, dt):
             _native.cfg_euler_(x, u, c, guidance_scale, dt)
@@ -291,14 +306,12 @@ def data_parallel_sample(dit, latents: torch.Tensor, prompt_embeds: torch.Tensor
             return zero, zero
 
     if use_apg:
-        nat_sums, nat_upd = _native_apg_ops()
-        sums = nat_sums if b else (lambda u, c, k, ph: torch.zeros(2, device=dev, dtype=torch.float32))
-        upd = nat_upd if b else (lambda *a: None)
         n_total = n_img * C * lh * lw
+        ws = torch.zeros(4, device=dev, dtype=torch.float32)
 
-        def combine(x, u, c, dt):
-            apg_step(x, u, c, dt, guidance_scale, apg.orthogonal_threshold, n_total, sums, upd,
-                     reduce=lambda t: all_reduce_sum_(t, group))
+        def combine(x, u, c, dt):  # two 2-float all-reduces per step, on the device (no .tolist())
+            apg_step_device(x, u, c, dt, guidance_scale, apg.orthogonal_threshold, n_total, ws,
+                            reduce=lambda t: all_reduce_sum_(t, group))
     else:
         def combine(x, u, c, dt):
             if b:

@@ -18,10 +18,13 @@ accepted too. A target entry t matches a module named t or ending in "." + t, as
 """
 from __future__ import annotations
 
+import logging
 import re
 from typing import Dict, Iterable, Optional, Tuple
 
 import torch
+
+logger = logging.getLogger(__name__)
 
 _KEY = re.compile(r"^(?P<mod>.+)\.lora_(?P<ab>[AB])(?:\.[^.]+)?\.weight$")
 
@@ -50,18 +53,28 @@ def _targeted(name: str, targets: Optional[Iterable[str]]) -> bool:
 @torch.no_grad()
 def merge_lora_(model: torch.nn.Module, state_dict: Dict[str, torch.Tensor], scaling: float = 1.0,
                 target_modules: Optional[Iterable[str]] = None, rank: Optional[int] = None) -> int:
-    """Fold every adapter of `state_dict` into `model` in place: W <- W + scaling * B @ A. Returns the number of
-    merged modules. Every adapter must name an nn.Linear of the model that `target_modules` selects, with
-    matching shapes (and rank `rank` when given) -- peft's set_peft_model_state_dict would not load it either."""
+    """Fold every adapter of `state_dict` into `model` in place: W <- W_base + scaling * B @ A. Returns the number of
+    merged modules.
+
+    Loading REPLACES, as peft's set_peft_model_state_dict does for the model's one ("default") adapter
+    (/root/reference/f_lite/model.py:492-495, pt.py:123-126): a module that already carries a merged adapter is
+    first restored to its base weight (kept on the host at the first merge), so loading the same file twice leaves
+    the weights bit-identical, and a second adapter does not stack on the first. Modules the new file does not name
+    keep the adapter they had, as peft's do. If a merged weight was overwritten since (load_state_dict, random_init_),
+    its current value is taken as the new base.
+
+    Adapters on modules that do not exist or that `target_modules` does not select are skipped with a warning (peft
+    loads with strict=False and reports them as unexpected keys). A shape or rank mismatch raises: peft would
+    refuse to copy such a tensor too."""
     targets = None if target_modules is None else [t.strip() for t in target_modules if t.strip()]
     modules = dict(model.named_modules())
     pairs = lora_pairs(state_dict)
+    todo, skipped = [], []
     for mod, (A, B) in pairs.items():
         lin = modules.get(mod)
-        if not isinstance(lin, torch.nn.Linear):
-            raise KeyError(f"LoRA adapter for {mod!r}: no such Linear in the model")
-        if not _targeted(mod, targets):
-            raise KeyError(f"LoRA adapter for {mod!r} is not among the target modules {targets}")
+        if not isinstance(lin, torch.nn.Linear) or not _targeted(mod, targets):
+            skipped.append(mod)
+            continue
         W = lin.weight
         r = A.shape[0]
         if A.shape != (r, W.shape[1]) or B.shape != (W.shape[0], r):
@@ -69,6 +82,32 @@ def merge_lora_(model: torch.nn.Module, state_dict: Dict[str, torch.Tensor], sca
                              f"{tuple(W.shape)}")
         if rank is not None and r != rank:
             raise ValueError(f"LoRA rank of {mod!r} is {r}, lora_rank says {rank}")
+        todo.append((mod, lin, A, B))
+    if skipped:
+        logger.warning("LoRA: skipped %d adapter(s) on modules that are missing or not targeted (%s): %s",
+                       len(skipped), targets, ", ".join(sorted(skipped)[:8]) + (" ..." if len(skipped) > 8 else ""))
+    merged = getattr(model, "_lora_merged", None)
+    if merged is None:
+        merged = {}
+        object.__setattr__(model, "_lora_merged", merged)
+    for mod, lin, A, B in todo:
+        W = lin.weight
+        rec = merged.get(mod)
+        if rec is not None and rec["version"] == W._version and rec["ptr"] == W.data_ptr():
+            base = rec["base"]  # the weight still holds our merge: start from the kept base
+        else:
+            base = W.detach().to("cpu", copy=True)
         delta = B.to(W.device, torch.float32) @ A.to(W.device, torch.float32)
-        W.copy_((W.float() + scaling * delta).to(W.dtype))
-    return len(pairs)
+        W.copy_((base.to(W.device, torch.float32) + scaling * delta).to(W.dtype))
+        merged[mod] = {"A": A.detach().cpu(), "B": B.detach().cpu(), "scaling": scaling, "base": base,
+                       "version": W._version, "ptr": W.data_ptr()}
+    return len(todo)
+
+
+def merged_state_dict(model: torch.nn.Module) -> Dict[str, torch.Tensor]:
+    """The adapters currently merged into `model`, as a peft state dict ("<module>.lora_A.weight" / "lora_B")."""
+    out = {}
+    for mod, rec in sorted(getattr(model, "_lora_merged", {}).items()):
+        out[f"{mod}.lora_A.weight"] = rec["A"]
+        out[f"{mod}.lora_B.weight"] = rec["B"]
+    return out

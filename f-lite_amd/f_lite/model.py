@@ -192,6 +192,14 @@ class DiT(nn.Module):
         self._wgen += 1  # written through raw pointers: no version bump
         return self
 
+    def weights_updated(self):
+        """Declare that parameters were written behind autograd's version counters -- through `p.data` (a
+        `p.data.copy_(...)` gets a fresh counter) or through raw device pointers: the engine re-derives its copies
+        (MXFP8 weights, the cross-attention K/V cache) before its next run. Writes through the parameters
+        themselves (load_state_dict, `p.copy_` under no_grad) are seen without this call."""
+        self._wgen += 1
+        return self
+
     @property
     def dtype(self):
         return next(self.parameters()).dtype
@@ -251,15 +259,15 @@ class DiT(nn.Module):
         from .lora import merge_lora_
 
         sd = torch.load(str(Path(load_directory) / "lora_weights.pt"), map_location="cpu", weights_only=True)
-        n = merge_lora_(self, sd, scaling=1.0, target_modules=target_modules)
-        self._lora_state_dict = sd
-        return n
+        return merge_lora_(self, sd, scaling=1.0, target_modules=target_modules)
 
     def save_lora_weights(self, save_directory):
-        """`<save_directory>/lora_weights.pt`: the adapter last merged by load_lora_weights / load_f_lite_pt (the
-        weights hold it merged, so there is no separate adapter to read back, unlike the reference's peft one)."""
-        sd = getattr(self, "_lora_state_dict", None)
-        if sd is None:
+        """`<save_directory>/lora_weights.pt`: the adapters merged by load_lora_weights / load_f_lite_pt, latest per
+        module (what get_peft_model_state_dict returns for peft's one adapter, model.py:487-490)."""
+        from .lora import merged_state_dict
+
+        sd = merged_state_dict(self)
+        if not sd:
             raise RuntimeError("no LoRA adapter has been loaded into this model")
         torch.save(sd, f"{save_directory}/lora_weights.pt")
 
@@ -319,13 +327,16 @@ class DiT(nn.Module):
         self._bound = (ptrs, vers)
         return self._engine
 
-    def enable_fp8(self, enabled: bool = True):
+    def enable_fp8(self, enabled: bool = True, bf16_blocks=()):
         """BASELINE.json configs[4]: run every block GEMM (qkv, proj, cross q / proj, SwiGLU gate-up, down) on
         MXFP8 weights and activations (OCP e4m3, E8M0 scale per 32 K elements) on the gfx950 block-scaled MFMA.
-        The bf16 parameters stay the source of truth; the engine quantises them once. No reference counterpart
-        (the reference runs bf16 only)."""
+        The bf16 parameters stay the source of truth; the engine quantises them once. `bf16_blocks`: block indices
+        that keep their bf16 GEMMs (a precision policy, e.g. (0, depth - 1); DESIGN §4 prices each). No reference
+        counterpart (the reference runs bf16 only)."""
         self._fp8 = bool(enabled)
-        self.engine().enable_fp8(self._fp8, self.device)
+        eng = self.engine()
+        eng.set_fp8_bf16_blocks(bf16_blocks)
+        eng.enable_fp8(self._fp8, self.device)
         return self
 
     # ------------------------------------------------------------------ forward

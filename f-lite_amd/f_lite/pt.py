@@ -102,7 +102,6 @@ def load_f_lite_pt(
         logger.info("Loading LoRA weights from %s", lora_path)
         lsd = torch.load(str(lora_path), map_location="cpu", weights_only=True)
         merge_lora_(dit, lsd, scaling=1.0, target_modules=lora_target_modules.split(","), rank=lora_rank)
-        dit._lora_state_dict = lsd
         logger.info("Successfully loaded LoRA weights with scale %s", lora_scale)
     vae = None
     if vae_path is not None:

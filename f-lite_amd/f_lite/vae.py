@@ -223,6 +223,12 @@ class AutoencoderKL(nn.Module):
         save_file({k: v.detach().contiguous().cpu() for k, v in self.state_dict().items()},
                   str(p / "diffusion_pytorch_model.safetensors"))
 
+    def weights_updated(self):
+        """Declare that parameters were written behind autograd's version counters (through `p.data` or raw device
+        pointers): the engine re-packs its conv weights before the next decode."""
+        self._wgen += 1
+        return self
+
     @property
     def dtype(self):
         return next(self.parameters()).dtype

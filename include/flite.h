@@ -256,6 +256,17 @@ int flite_apg_sums(void* stream, const float* uncond, const float* cond, long n,
 int flite_apg_euler(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
                     float k, float orth_scale, float dt);
 /*
+ * The same APG split with the scalars kept on the device (no host round trip per step; replaces the host algebra
+ * between pipeline.py:281 and :285). ws4 = 4 device floats: flite_apg_sums_dev(phase 0) writes ws4[0..1] = [sum
+ * c (c - u), sum c^2]; phase 1 derives k = ws4[0] / ws4[1] and writes ws4[2..3] = [sum o, sum o^2]. Between the
+ * phases the caller may all-reduce ws4[0..1] (resp. ws4[2..3]) in place on the same stream order.
+ * flite_apg_euler_dev derives k and orth_scale = min(1, threshold / std) (unbiased std over n_total elements, the
+ * whole reference batch) from ws4 with the fp32 expressions of flite_dit_sample's APG kernel, then updates acc.
+ */
+int flite_apg_sums_dev(void* stream, const float* uncond, const float* cond, long n, int phase, float* ws4);
+int flite_apg_euler_dev(void* stream, const float* uncond, const float* cond, float* acc, long n, float guidance,
+                        float threshold, long n_total, const float* ws4, float dt);
+/*
  * fp8 mode (BASELINE.json configs[4]): enable=1 quantises every bound block GEMM weight (qkv, proj, cross q /
  * proj, SwiGLU gate|up, down) once into engine-owned MXFP8 copies and runs those GEMMs on the block-scaled fp8
  * MFMA with MXFP8 activations (RMSNorm+modulate, attention output and SwiGLU output quantised where they are
@@ -264,6 +275,12 @@ int flite_apg_euler(void* stream, const float* uncond, const float* cond, float*
  * keeps fp8 mode on: the next flite_dit_forward / flite_dit_sample requantises before it runs.
  */
 int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable);
+/*
+ * fp8 precision policy: the `n` listed blocks keep the bf16 GEMMs (run as in bf16 mode) while fp8 mode is on; the
+ * others run MXFP8. n = 0 (the default) puts every block on fp8. Blocks are self-contained between residual-stream
+ * reads and writes (fp32), so any mix is valid. No reference counterpart (the reference is bf16 only).
+ */
+int flite_dit_set_fp8_bf16_blocks(flite_dit* dit, const int* blocks, int n);
 /*
  * The CONTENTS of bound weights changed in place (a load_state_dict copy, a LoRA merge, re-initialisation):
  * every engine-owned copy derived from them is remade -- in fp8 mode the MXFP8 weights are requantised on

@@ -159,3 +159,39 @@ def test_apg_split_kernels_match_single_launch():
     orth = dd - (dy * dd).sum() / (dy * dy).sum() * dy
     want = acc.double() + 0.05 * (dy + (G - 1) * orth * min(1.0, 0.03 / orth.std().item()))
     torch.testing.assert_close(got.cpu().double(), want, rtol=1e-4, atol=1e-5)
+
+
+def test_apg_device_scalars_match_host_algebra():
+    """distributed.apg_step_device (flite_apg_sums_dev / flite_apg_euler_dev: k and the orthogonal scale derived on
+    the device, no host round trip) == apg_step's host fp32 algebra to rounding, == the reference expression, and a
+    split of the batch over two "ranks" whose partial sums are added in place reproduces the whole-batch step."""
+    from f_lite.distributed import apg_step, apg_step_device
+
+    g = torch.Generator().manual_seed(5)
+    u = torch.randn(3, 16, 64, 64, generator=g)
+    c = u + 0.2 * torch.randn(3, 16, 64, 64, generator=g)
+    acc = torch.randn(3, 16, 64, 64, generator=g)
+    host = acc.cuda()
+    apg_step(host, u.cuda(), c.cuda(), 0.05, G, 0.03, u.numel(), _native.apg_sums,
+             lambda a, uu, cc, gs, k, sc, dt: _native.apg_euler_(a, uu, cc, gs, k, sc, dt))
+    dev = acc.cuda()
+    ws = torch.zeros(4, device="cuda")
+    apg_step_device(dev, u.cuda(), c.cuda(), 0.05, G, 0.03, u.numel(), ws)
+    torch.testing.assert_close(dev, host, rtol=1e-6, atol=1e-6)
+    dy, dd = c.double(), (c - u).double()
+    orth = dd - (dy * dd).sum() / (dy * dy).sum() * dy
+    want = acc.double() + 0.05 * (dy + (G - 1) * orth * min(1.0, 0.03 / orth.std().item()))
+    torch.testing.assert_close(dev.cpu().double(), want, rtol=1e-4, atol=1e-5)
+    # two shards (images {0, 2} and {1}); "reduce" adds the other shard's partial sums in place
+    parts = [[0, 2], [1]]
+    accs = [acc[p].cuda() for p in parts]
+    wss = [torch.zeros(4, device="cuda") for _ in parts]
+    for phase in (0, 1):
+        for p, w in zip(parts, wss):
+            _native.apg_sums_dev(u[p].cuda(), c[p].cuda(), phase, w)
+        tot = wss[0][2 * phase: 2 * phase + 2] + wss[1][2 * phase: 2 * phase + 2]
+        for w in wss:
+            w[2 * phase: 2 * phase + 2] = tot
+    for p, a, w in zip(parts, accs, wss):
+        _native.apg_euler_dev_(a, u[p].cuda(), c[p].cuda(), G, 0.03, u.numel(), w, 0.05)
+        torch.testing.assert_close(a.cpu().double(), want[p], rtol=1e-4, atol=1e-5)

@@ -212,3 +212,63 @@ def test_qk_norm_fusion_matches_separate_kernel(tmp_path):
     p = psnr(outs[0], outs[1])
     print(f"fused vs separate RoPE/QK-norm (10B layout, depth 2, 512^2): {p:.2f} dB")
     assert p >= 45.0
+
+
+_DEDUP_SCRIPT = """
+import sys, torch
+sys.path[:0] = [{pkg!r}, {root!r}]
+from f_lite import DiT, FLitePipeline
+from f_lite.model import PRESETS
+out = {{}}
+for name, cfg, hw, fp8 in (("tiny", dict(PRESETS["tiny"]), 128, False),
+                           ("10b_d2", dict(PRESETS["10b"], depth=2), 256, False),
+                           ("10b_d2_fp8", dict(PRESETS["10b"], depth=2), 256, True)):
+    m = DiT.random(seed=0, device="cuda", **cfg)
+    if fp8:
+        m.enable_fp8(True)
+    g = torch.Generator().manual_seed(4)
+    lat = torch.randn(2, 16, hw // 8, hw // 8, generator=g).bfloat16().cuda()
+    pos = torch.randn(2, 24, cfg["cross_attn_input_size"], generator=g).bfloat16().cuda()
+    for graph in (False, True):
+        out[f"{{name}}.{{graph}}"] = FLitePipeline(m)(prompt_embeds=pos, latents=lat, height=hw, width=hw,
+            num_inference_steps=4, guidance_scale=6.0, output_type="latent", use_graph=graph).images.float().cpu()
+    out[f"{{name}}.lat"] = lat.float().cpu()
+    out[f"{{name}}.pos"] = pos.float().cpu()
+torch.save(out, sys.argv[1])
+"""
+
+
+def test_cfg_block0_dedup_matches_full_batch(tmp_path):
+    """dit.cpp forward: with a CFG batch, block 0's self-attention sub-block runs once per image and its residual
+    rows are copied to the other CFG copy (rows are dup-major: [copy][image]). Two images per launch, bf16 and
+    MXFP8, eager and hipGraph, against FLITE_NO_CFG_DEDUP=1 (every copy computed; a child process each, the switch
+    is read once per process) and, for the tiny bf16 model, against the fp32 oracle's batched CFG loop."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    script = tmp_path / "dedup.py"
+    script.write_text(_DEDUP_SCRIPT.format(pkg=str(root / "f-lite_amd"), root=str(root)))
+    outs = []
+    for i, extra in enumerate(({}, {"FLITE_NO_CFG_DEDUP": "1"})):
+        f = tmp_path / f"o{i}.pt"
+        r = subprocess.run([sys.executable, str(script), str(f)], env=dict(os.environ, **extra), capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(torch.load(f, weights_only=True))
+    dd, full = outs
+    for name in ("tiny", "10b_d2", "10b_d2_fp8"):
+        assert torch.equal(dd[f"{name}.False"], dd[f"{name}.True"])  # graph == eager with the dedup
+        p = psnr(dd[f"{name}.True"], full[f"{name}.True"])
+        print(f"CFG dedup vs full batch, {name}, 2 images per launch: {p:.2f} dB")
+        assert p >= 50.0
+        # the two images differ (a copy-loop indexing error would duplicate one image into the other)
+        assert psnr(dd[f"{name}.True"][0], dd[f"{name}.True"][1]) < 30.0
+    ref = R.sample(R.RefDiT.random(R.PRESETS["tiny"], dtype=torch.float32), dd["tiny.lat"], dd["tiny.pos"],
+                   torch.zeros_like(dd["tiny.pos"]), num_steps=4, guidance_scale=6.0, apg=R.APG(enabled=False),
+                   height=128, width=128, t_dtype=torch.bfloat16, acc_dtype=torch.float32)
+    p = psnr(dd["tiny.True"], ref)
+    print(f"CFG dedup, tiny, 2 images: {p:.2f} dB vs the fp32 oracle")
+    assert p >= 35.0

@@ -263,3 +263,48 @@ def test_256_free_running_30_steps(gold3, m7b, m10b, name, g):
     assert p >= floor
     if g == 1.0:
         assert p >= 40.0
+
+
+# ---- the METRIC configuration pinned end to end (tests/golden/make_golden_full4.py) ----
+@pytest.fixture(scope="module")
+def gold4():
+    from safetensors.torch import load_file
+
+    f = GOLD / "golden_full4.safetensors"
+    if not f.exists():
+        pytest.skip("golden_full4.safetensors not generated")
+    return load_file(str(f)), json.loads((GOLD / "golden_full4_meta.json").read_text())
+
+
+@pytest.mark.parametrize("g", [6.0, 1.0])
+def test_10b_1024_30_steps_vs_reference(gold4, m10b, g):
+    """BASELINE's metric workload end to end against the reference itself: 10B (model_v2 layout), 1024^2, 30 steps,
+    the hipGraph-captured loop the bench times. P3 final latents vs the reference's fp32 trajectory, beside (and
+    above) the reference's own bf16 run; at CFG 1 the SURVEY §8d bar of 40 dB. Then the uint8 image of the product
+    path (HIP loop + HIP VAE) vs oracle/vae_ref.py's decode of the reference's fp32 latents, >= 40 dB (peak 255)."""
+    from f_lite.vae import AutoencoderKL
+
+    gd, meta = gold4
+    key = f"10b.1024.s30.g{g:g}"
+    if f"{key}.f32.final" not in gd:
+        pytest.skip(f"{key} not in the fixture file yet")
+    pipe = FLitePipeline(m10b, vae=AutoencoderKL.random(seed=0))
+    assert (pipe.vae.config.scaling_factor, pipe.vae.config.shift_factor) == (SCALING, SHIFT)
+    kw = dict(prompt_embeds=hashed(meta, "ctx"), latents=hashed(meta, "latents_1024"), height=1024, width=1024,
+              num_inference_steps=30, guidance_scale=g, use_graph=True)
+    lat = pipe(**kw, output_type="latent").images.float()
+    p = psnr(lat / SCALING + SHIFT, gd[f"{key}.f32.final"])
+    floor = meta.get(f"{key}.bf16_vs_f32_psnr")
+    print(f"10B 1024^2 30-step CFG-{g:g} final latents: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
+          f"{'n/a' if floor is None else f'{floor:.2f} dB'})")
+    if floor is not None:
+        assert p >= floor
+    if g == 1.0:
+        assert p >= 40.0
+    if f"{key}.f32.image" in gd:
+        img = pipe(**kw, output_type="uint8").images.cpu()
+        ref = gd[f"{key}.f32.image"]
+        assert img.shape == ref.shape == (1, 1024, 1024, 3)
+        pi = 10 * math.log10(255.0 ** 2 / max((img.double() - ref.double()).pow(2).mean().item(), 1e-12))
+        print(f"  uint8 image (HIP loop + HIP VAE) vs oracle VAE on the reference latents: {pi:.2f} dB")
+        assert pi >= 40.0

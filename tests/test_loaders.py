@@ -142,7 +142,8 @@ def test_lora_merge(preset):
 
 def test_lora_pt_loader_and_dit_methods(tmp_path):
     """load_f_lite_pt(lora_path=...) (pt.py:107-135) and DiT.load_lora_weights / save_lora_weights
-    (model.py:487-495) give the same merged weights; wrong rank, untargeted or half-paired adapters raise."""
+    (model.py:487-495) give the same merged weights; a wrong rank or a half-paired adapter raises, an untargeted one
+    is skipped."""
     from f_lite.lora import merge_lora_
     from f_lite.pt import load_f_lite_pt
 
@@ -164,13 +165,66 @@ def test_lora_pt_loader_and_dit_methods(tmp_path):
     assert all(torch.equal(fresh.state_dict()[k], v) for k, v in got.items())
     with pytest.raises(ValueError):  # lora_rank disagrees with the file (peft would refuse the shapes)
         load_f_lite_pt(tmp_path / "model.pt", "cpu", lora_path=tmp_path / "lora.pt", lora_rank=4, **kw)
-    with pytest.raises(KeyError):  # an adapter on a module outside lora_target_modules
-        load_f_lite_pt(tmp_path / "model.pt", "cpu", lora_path=tmp_path / "lora.pt", lora_rank=8,
-                       lora_target_modules="qkv", **kw)
+    # an adapter on a module outside lora_target_modules is skipped with a warning (peft's strict=False load)
+    only_qkv = load_f_lite_pt(tmp_path / "model.pt", "cpu", dtype="bfloat16", lora_path=tmp_path / "lora.pt",
+                              lora_rank=8, lora_target_modules="qkv", **kw).dit_model
+    base = load_f_lite_pt(tmp_path / "model.pt", "cpu", dtype="bfloat16", **kw).dit_model.state_dict()
+    for k, v in only_qkv.state_dict().items():
+        assert torch.equal(v, got[k] if k.endswith("self_attn.qkv.weight") else base[k]), k
     half = {k: v for k, v in lsd.items() if not k.startswith("blocks.0.self_attn.qkv.lora_B")}
     assert len(half) == len(lsd) - 1
     with pytest.raises(KeyError):
         merge_lora_(fresh, half)
+
+
+def test_lora_load_replaces_like_peft(tmp_path):
+    """loading an adapter REPLACES the merged one per module, as set_peft_model_state_dict does for
+    peft's one adapter (model.py:492-495): the same file twice leaves the weights bit-identical, a second adapter
+    does not stack on the first, modules the second file omits keep the first adapter, and save_lora_weights
+    writes the union (latest per module)."""
+    from f_lite.lora import merge_lora_
+
+    m = _filled(DiT, "tiny").to(torch.bfloat16)
+    base = {k: v.clone() for k, v in m.state_dict().items()}
+    a1 = _lora_sd(m, rank=4, seed=1)
+    torch.save(a1, tmp_path / "lora_weights.pt")
+    m.load_lora_weights(tmp_path)
+    once = {k: v.clone() for k, v in m.state_dict().items()}
+    m.load_lora_weights(tmp_path)
+    assert all(torch.equal(m.state_dict()[k], v) for k, v in once.items())
+    # a second adapter on the qkv modules only: qkv = base + B2 A2, the rest keeps adapter 1
+    a2 = _lora_sd(m, targets=("qkv",), rank=4, seed=2)
+    merge_lora_(m, a2)
+    for k, v in m.state_dict().items():
+        mod = k[: -len(".weight")]
+        if f"{mod}.lora_A.weight" in a2:
+            want = (base[k].float() + a2[f"{mod}.lora_B.weight"] @ a2[f"{mod}.lora_A.weight"]).bfloat16()
+            assert torch.equal(v, want), k
+        else:
+            assert torch.equal(v, once[k]), k
+    m.save_lora_weights(tmp_path)
+    saved = torch.load(tmp_path / "lora_weights.pt", weights_only=True)
+    assert set(saved) == set(a1)
+    for k, v in saved.items():
+        assert torch.equal(v, (a2 if k in a2 else a1)[k]), k
+    # a weight overwritten since the merge (load_state_dict) becomes the new base
+    m.load_state_dict(base)
+    merge_lora_(m, a2)
+    k = next(k for k in a2 if k.endswith("lora_A.weight")).replace(".lora_A.weight", "")
+    want = (base[k + ".weight"].float() + a2[k + ".lora_B.weight"] @ a2[k + ".lora_A.weight"]).bfloat16()
+    assert torch.equal(m.state_dict()[k + ".weight"], want)
+
+
+def test_weights_updated_bumps_generation():
+    m = _filled(DiT, "tiny")
+    g = m._wgen
+    assert m.weights_updated() is m and m._wgen == g + 1
+    from f_lite.vae import AutoencoderKL
+
+    v = AutoencoderKL(block_out_channels=(32, 32), layers_per_block=1, norm_num_groups=8)
+    g = v._wgen
+    v.weights_updated()
+    assert v._wgen == g + 1
 
 
 def test_generate_signature_matches_reference():
