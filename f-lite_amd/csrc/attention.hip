@@ -359,9 +359,21 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     using I1 = std::integral_constant<int, 1>;
     using BT = std::integral_constant<bool, true>;
     using BF = std::integral_constant<bool, false>;
-    auto rsrc_tile = [&](const bf16_t* base, long off, long stride, int t, bool live) {
-      const long rows_left = live ? k_len - (long)t * KT : 0;
-      return make_rsrc(base + off + (long)t * KT * stride, (unsigned)max(0L, min(rows_left * stride * 2, 0x7fffffffL)));
+    // Descriptor of key tile t: base + t * tile_bytes, range = the sequence's bytes left (0 when dead). The tile
+    // stride and the total are kernel constants, so a descriptor is a 32x32-bit product, a 64-bit add and a
+    // clamp (the 64-bit multiplies and compares of the general form cost ~50 scalar instructions per iteration
+    // at the loop head, with the MFMA pipe idle behind the barrier).
+    const unsigned k_tile_b = (unsigned)(KT * p.k_row_stride * 2), v_tile_b = (unsigned)(KT * p.v_row_stride * 2);
+    const long k_total_b = (long)k_len * p.k_row_stride * 2, v_total_b = (long)k_len * p.v_row_stride * 2;
+    const char* k_ptr0 = (const char*)(p.k + k_base);
+    const char* v_ptr0 = (const char*)(p.v + v_base);
+    auto rsrc_tile = [&](const char* base, unsigned tile_b, long total_b, int t, bool live) {
+      const unsigned long off = (unsigned long)(unsigned)t * tile_b;
+      const long left = total_b - (long)off;
+      const int hi = (int)(left >> 32);  // 32-bit compares only (gfx950 has no 64-bit scalar less-than)
+      const unsigned lo = (unsigned)left;
+      const unsigned range = (!live || hi < 0) ? 0u : (hi > 0 || lo > 0x7fffffffu) ? 0x7fffffffu : lo;
+      return make_rsrc(base + off, range);
     };
     constexpr int KAHEAD = 3;  // K fragment reads issued this many k-steps ahead of their MFMA pair
     constexpr int VAHEAD = 4;  // V^T transposed reads issued this many MFMAs ahead
@@ -374,8 +386,8 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       const char* Kb = kbase + KB * TILE;
       i32x4 krs = {0, 0, 0, 0}, vrs = {0, 0, 0, 0};
       if constexpr (DMA) {
-        krs = rsrc_tile(p.k, k_base, p.k_row_stride, tk, k_live);
-        vrs = rsrc_tile(p.v, v_base, p.v_row_stride, tv, v_live);
+        krs = rsrc_tile(k_ptr0, k_tile_b, k_total_b, tk, k_live);
+        vrs = rsrc_tile(v_ptr0, v_tile_b, v_total_b, tv, v_live);
       }
       bf16x8 k0[16], k1[16];
 #pragma unroll
@@ -476,7 +488,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       // prologue: K_0, V_0 into buffer 0 and K_1 into Kbuf 1; S_0 and its softmax into pa
       stage(t_begin, 0);
       {
-        const i32x4 krs = rsrc_tile(p.k, k_base, p.k_row_stride, t_begin + 1, nt > 1);
+        const i32x4 krs = rsrc_tile(k_ptr0, k_tile_b, k_total_b, t_begin + 1, nt > 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) blds16(krs, k_src[i], lds0 + TILE + (wave * 8 + i) * 1024 + K_OFF);
       }

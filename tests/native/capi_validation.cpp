@@ -121,6 +121,11 @@ static void engine_binds(int per_block, int bias) {
   EXPECT_OK(eng.check_bound());
   EXPECT_OK(eng.bind(inv[0].first, p, inv[0].second));  // rebinding the same storage is accepted
   EXPECT_OK(eng.weights_updated(nullptr));               // bf16 mode: nothing derived
+  const int blks[2] = {0, c.depth};
+  EXPECT_ERR(eng.set_fp8_bf16_blocks(blks, 2), "out of range");
+  EXPECT_ERR(eng.set_fp8_bf16_blocks(nullptr, 1), "bad block list");
+  EXPECT_OK(eng.set_fp8_bf16_blocks(blks, 1));
+  EXPECT_OK(eng.set_fp8_bf16_blocks(nullptr, 0));
   EXPECT_ERR(eng.forward(nullptr, p, false, 1, 2, 0, 0), "prepare first");
   EXPECT_ERR(eng.unpatchify_out(nullptr, nullptr, false), "prepare first");
   long a = 0, b = 0;
@@ -155,6 +160,12 @@ int main() {
   EXPECT_ERR(flite_apg_sums(nullptr, nullptr, f, 4, 0.f, 0, f), "null");
   EXPECT_ERR(flite_apg_sums(nullptr, f, f, 4, 0.f, 2, f), "phase");
   EXPECT_ERR(flite_apg_euler(nullptr, f, f, nullptr, 4, 6.f, 0.f, 1.f, 0.1f), "null");
+  EXPECT_ERR(flite_apg_sums_dev(nullptr, f, f, 4, 0, nullptr), "null");
+  EXPECT_ERR(flite_apg_sums_dev(nullptr, f, f, -1, 0, f), "negative");
+  EXPECT_ERR(flite_apg_sums_dev(nullptr, f, f, 4, 3, f), "phase");
+  EXPECT_ERR(flite_apg_euler_dev(nullptr, f, f, f, 4, 6.f, 0.03f, 4, nullptr, 0.1f), "null");
+  EXPECT_ERR(flite_apg_euler_dev(nullptr, f, f, f, 8, 6.f, 0.03f, 4, f, 0.1f), "element counts");
+  EXPECT_ERR(flite_dit_set_fp8_bf16_blocks(nullptr, nullptr, 0), "null");
   // GEMM shape / stride / alignment validation happens before any kernel initialisation
   alignas(16) static char g[256];
   EXPECT_ERR(flite_gemm_bf16(nullptr, 0, 64, 64, g, 64, g, 64, nullptr, nullptr, 0, g, 64, nullptr, 0, 0), "empty");

@@ -117,6 +117,25 @@ def test_flop_accounting_matches_survey():
     assert abs(decoder_flops(1024, 1024) / 1e12 - 10.47) < 0.01
 
 
+def test_cpu_baseline_threads_follow_cgroup_quota(monkeypatch):
+    """bench.cpu_threads: every CPU the cgroup quota grants, else the affinity set capped by
+    OMP_NUM_THREADS, with the reason recorded."""
+    import bench
+
+    info = {"affinity_cores": 256, "cgroup_cpus": 16.0, "cgroup_cpu_max": "cpu.max: 1600000 100000"}
+    monkeypatch.setattr(bench, "host_info", lambda: dict(info))
+    n, why = bench.cpu_threads()
+    assert n == 16 and "quota grants 16" in why
+    info.update(cgroup_cpus=None, cgroup_cpu_max="cpu.max: max 100000")
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    n, why = bench.cpu_threads()
+    assert n == 16 and "OMP_NUM_THREADS=16" in why
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.cpu_threads()[0] == 256
+    q = bench.cgroup_cpu_quota()
+    assert set(q) == {"cgroup_cpu_max", "cgroup_cpus"}
+
+
 class _PointwiseDecoder:
     """Stand-in decoder whose pixel (y, x) depends only on latent (y // 8, x // 8): any correct tiling of it
     (grid, in-place blends of equal overlaps, crops, concatenation) reproduces the untiled output exactly."""
