@@ -17,8 +17,9 @@ Fixtures (tests/golden/golden_full4.safetensors) + golden_full4_meta.json:
   10b.1024.s30.g6.bf16.final   the same run in the reference's bf16 arithmetic (its own floor vs fp32)
   10b.1024.s30.g1.f32.final    CFG 1 (pipeline.py:248: guidance >= 1 still runs the CFG batch), fp32
   10b.1024.s30.g1.bf16.final   CFG 1, bf16 (when time allows)
-  {key}.f32.image              uint8 [1, 1024, 1024, 3]: oracle/vae_ref.py (the restated Flux decoder, seed-0
-                               generator weights) on the reference's fp32 final latents + pipeline.py:324-326
+  {key}.image                  uint8 [1, 1024, 1024, 3]: oracle/vae_ref.py (the restated Flux decoder, seed-0
+                               generator weights) on that trajectory's final latents + pipeline.py:324-326; the
+                               bf16 runs' images give the reference's own image-space floor (meta *.image_bf16_vs_f32)
 
 CFG 1 shortcut (stated): at guidance 1 pipeline.py:290 forms uncond + 1 * (cond - uncond). The wrapper below runs
 the reference DiT on the cond half only and hands the pipeline [cond, cond], so the combination returns cond
@@ -35,6 +36,7 @@ sys.dont_write_bytecode = True
 import argparse  # noqa: E402
 import hashlib  # noqa: E402
 import json  # noqa: E402
+import math  # noqa: E402
 import time  # noqa: E402
 from pathlib import Path  # noqa: E402
 
@@ -166,10 +168,18 @@ def main():
                 save()
     if not args.no_image:
         for key, _, dt, _ in TRAJ:
-            if dt == torch.float32 and f"{key}.final" in T and f"{key}.image" not in T:
+            if f"{key}.final" in T and f"{key}.image" not in T:
                 log(f"{key}: oracle VAE decode")
                 T[f"{key}.image"] = vae_oracle_image(T[f"{key}.final"])
                 save()
+        for key, _, dt, _ in TRAJ:  # the reference's own bf16 floor in image space (P3 image metric)
+            base = key.rsplit(".", 1)[0]
+            if dt == torch.bfloat16 and f"{key}.image" in T and f"{base}.f32.image" in T:
+                a, b = T[f"{key}.image"].double(), T[f"{base}.f32.image"].double()
+                meta[f"{base}.image_bf16_vs_f32_psnr"] = 10 * math.log10(255.0 ** 2 / max((a - b).pow(2).mean().item(),
+                                                                                        1e-12))
+                log(f"  {base} reference bf16 vs fp32 image: {meta[f'{base}.image_bf16_vs_f32_psnr']:.2f} dB")
+        save()
 
 
 if __name__ == "__main__":
