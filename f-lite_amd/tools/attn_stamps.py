@@ -19,8 +19,8 @@ sys.path.insert(0, str(HERE.parent))
 NV = 8  # values per wave
 
 
-def patch():
-    src = (HERE.parent / "csrc" / "attention.hip").read_text()
+def patch(src_path=None, name="stamps"):
+    src = Path(src_path or (HERE.parent / "csrc" / "attention.hip")).read_text()
 
     def sub(old, new, count=1):
         nonlocal src
@@ -84,8 +84,8 @@ def patch():
 ''')
     out = HERE / "variants" / "_src"
     out.mkdir(parents=True, exist_ok=True)
-    (out / "attention_stamps.hip").write_text(src)
-    print(f"wrote {out / 'attention_stamps.hip'}")
+    (out / f"attention_{name}.hip").write_text(src)
+    print(f"wrote {out / f'attention_{name}.hip'}")
 
 
 def run():
@@ -127,4 +127,7 @@ def run():
 
 
 if __name__ == "__main__":
-    patch() if sys.argv[1] == "patch" else run()
+    if sys.argv[1] == "patch":  # patch [SOURCE NAME]: stamp another variant's source
+        patch(*sys.argv[2:4])
+    else:
+        run()

@@ -19,7 +19,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 
 
-def make(name, kspread=False, vdma_b=None, qscale=False):
+def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False):
     src = (HERE.parent / "csrc" / "attention.hip").read_text()
 
     def sub(old, new, count=1):
@@ -64,6 +64,14 @@ def make(name, kspread=False, vdma_b=None, qscale=False):
             "  float m_run = BOUNDED ? 0.f : -1e30f;")
         sub("      const float v = __builtin_amdgcn_exp2f(sacc[r] * sl2 - m_run);",
             "      const float v = __builtin_amdgcn_exp2f(sacc[r]);")
+    if ldelay:  # row sum: add the PREVIOUS element's p (same adds, same order: bit-identical), so the v_add no
+        # longer waits on the v_exp just issued (the trans -> VALU forwarding hazard cost an s_nop per element)
+        sub("      l_run += v;\n      if (e & 1) {", "      l_run += e_prev;\n      if (e & 1) {")
+        sub("        if constexpr (EX) softmax_elem(pn, m, e_prev);\n        __builtin_amdgcn_sched_barrier(0);\n      }\n",
+            "        if constexpr (EX) softmax_elem(pn, m, e_prev);\n        __builtin_amdgcn_sched_barrier(0);\n      }\n"
+            "      if constexpr (EX) l_run += e_prev;\n")
+        sub("        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);\n",
+            "        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);\n        l_run += e_prev;\n")
     if vdma_b is not None:
         sub('''    auto phase_b = [&](auto vb_, auto ex_, u32x4 (&pc)[4], u32x4 (&pn)[4]) {
       constexpr int VB = decltype(vb_)::value;
@@ -103,4 +111,4 @@ if __name__ == "__main__":
     vb = None
     if "--vdma-b" in a:
         vb = int(a[a.index("--vdma-b") + 1])
-    make(name, kspread="--kspread" in a, vdma_b=vb, qscale="--qscale" in a)
+    make(name, kspread="--kspread" in a, vdma_b=vb, qscale="--qscale" in a, ldelay="--ldelay" in a)

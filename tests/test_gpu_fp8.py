@@ -308,9 +308,12 @@ def gold3():
     return load_file(str(d / "golden_full3.safetensors")), json.loads((d / "golden_full3_meta.json").read_text())
 
 
-# measured on the MI355X (profiles/r04*); bars sit 3 dB under them. bf16 on the same fixtures: 37.72 / 35.47 dB at
-# CFG 6 and 56.28 / 56.56 dB at CFG 1 (7B / 10B, test_gpu_full_depth.py::test_256_free_running_30_steps)
-FP8_P3_BARS = {("7b", 6.0): 0.0, ("7b", 1.0): 0.0, ("10b", 6.0): 0.0, ("10b", 1.0): 0.0}
+# measured on the MI355X (profiles/r04a/pytest.log: 16.80 / 19.31 dB at CFG 6, 35.12 / 35.92 dB at CFG 1, 7B / 10B);
+# bars sit 3 dB under them. bf16 on the same fixtures: 37.72 / 35.47 dB at CFG 6 and 56.28 / 56.56 dB at CFG 1
+# (test_gpu_full_depth.py::test_256_free_running_30_steps); the reference's own bf16 run: 30.66 / 30.60 and
+# 47.51 / 48.21 dB. MXFP8's e4m3 elements carry 3 mantissa bits (bf16: 8), so its forward error is ~2^5 larger
+# and CFG 6 amplifies it over the trajectory (DESIGN §4, fp8 policies)
+FP8_P3_BARS = {("7b", 6.0): 13.8, ("7b", 1.0): 32.1, ("10b", 6.0): 16.3, ("10b", 1.0): 32.9}
 
 
 @pytest.mark.parametrize("name", ["7b", "10b"])
