@@ -49,6 +49,10 @@ constexpr long CNT_BYTES = 4096;  // counter block at the workspace start (1024 
 constexpr int MAX_SPLIT = 16;     // key ranges per tail
 constexpr int MIN_SPLIT_KEYS = 4 * KT;     // shorter key ranges: the tail round is cheaper than the hand-off
 constexpr int SPLIT_FIRST_KEYS = 16 * KT;  // below this the tail chunks go first (see attn_fwd)
+// The bounded path takes p = exp2(score * scale * log2 e) with no shift: a bound of 40 keeps p <= 2^57.7, every row
+// sum and every O accumulator far inside the fp32 range for any sequence length. Larger bounds take the online
+// softmax. (The DiT's QK-normed scores: 16.5, dit.cpp kQKNormScoreBound.)
+constexpr float kMaxBoundedScore = 40.f;
 
 __device__ __forceinline__ s16x4 ds_tr16(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(p));
@@ -127,7 +131,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
 
 // BOUNDED: every score s*scale is known to lie in [-max_score, max_score] (QK-normed q and k: |q|,|k| <= 16
 // for head_dim 256, so |q.k|/16 <= 16 -- model.py:180,197 precede every attention call of the DiT). Softmax is
-// shift-invariant, so the running max is replaced by the fixed bound: no row max, no O/l rescale, p <= 1.
+// shift-invariant and the bound keeps exp2 of the raw scaled score in range, so there is no running max, no O/l
+// rescale and no shift at all: p = exp2(s'), s' = q'.k with q' = q * scale * log2(e) (pre-scaled at load).
 template <bool BOUNDED>
 __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -191,7 +196,16 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     const bf16_t* qp = p.q + (long)(q_start + qc) * p.q_row_stride + (long)h * p.q_head_stride + 8 * hh;
 #pragma unroll
     for (int s = 0; s < 16; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
-    if constexpr (BOUNDED) {  // move Q^T into AGPRs here, then clear the write -> MFMA-read hazard
+    if constexpr (BOUNDED) {
+      // Scores in log2 units straight out of the MFMA: Q^T pre-scaled by scale * log2(e) (one bf16 rounding of
+      // q, ~0.1 % of a probability; the P operand's own bf16 rounding is 2-4x that), so each probability is a
+      // single v_exp (no v_fma per score: the PV + softmax phase is issue-bound, profiles/r04a/stamps.log)
+      const float qs = p.scale * 1.4426950408889634f;
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * qs);
+      // move Q^T into AGPRs here, then clear the write -> MFMA-read hazard
 #pragma unroll
       for (int s = 0; s < 16; ++s) asm volatile("" : "+a"(qf[s]));
       asm volatile("s_nop 4" ::: "memory");
@@ -234,7 +248,9 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) o_acc[i][r] = 0.f;
   const float sl2 = p.scale * 1.4426950408889634f;
-  float m_run = BOUNDED ? p.max_score * 1.4426950408889634f : -1e30f;
+  // bounded path: no shift at all (|s'| <= max_score * log2(e) keeps every p = exp2(s') and every sum far inside
+  // the fp32 range: attn_fwd admits max_score <= kMaxBoundedScore); online softmax: the running max
+  float m_run = BOUNDED ? 0.f : -1e30f;
   float l_run = 0.f;
 
   // per-lane LDS read bases (everything else is an immediate offset)
@@ -423,12 +439,14 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
       }
       mfma_read_fence(s0, s1);  // MFMA write of S -> VALU read (softmax in the next phase B)
     };
-    // softmax of key e (0..31: half e >> 4, row r = e & 15) of the pending S into the P^T operand pn
+    // softmax of key e (0..31: half e >> 4, row r = e & 15) of the pending S into the P^T operand pn. The row sum
+    // adds the PREVIOUS element's p (the caller adds the last one after the loop): the same adds in the same order,
+    // without the v_add waiting on the v_exp just issued (an s_nop per score for the trans -> VALU hazard)
     auto softmax_elem = [&](u32x4 (&pn)[4], int e, float& e_prev) {
       const f32x16& sacc = e < 16 ? s0 : s1;
       const int r = e & 15;
-      const float v = __builtin_amdgcn_exp2f(sacc[r] * sl2 - m_run);
-      l_run += v;
+      const float v = __builtin_amdgcn_exp2f(sacc[r]);
+      l_run += e_prev;
       if (e & 1) {
         const bf16x2 pr = {(__bf16)e_prev, (__bf16)v};
         pn[(e >> 4) * 2 + (r >> 3)][(r & 7) >> 1] = __builtin_bit_cast(unsigned, pr);
@@ -467,6 +485,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         if constexpr (EX) softmax_elem(pn, m, e_prev);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr (EX) l_run += e_prev;
     };
     // iteration j (parity P): phase A for S_{j+1} (HS) and phase B for PV_j with the softmax of S_{j+1}
     auto iter = [&](auto par_, auto hs_, int j) {
@@ -499,6 +518,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         float e_prev = 0.f;
 #pragma unroll
         for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);
+        l_run += e_prev;
       }
       __syncthreads();  // every wave's K_0 reads are done before iteration 0 refills Kbuf 0
       int j = 0;
@@ -534,7 +554,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
   }
 
   if constexpr (BOUNDED) o_acc_fence(o_acc);
-  // keys past the end were staged as zero rows: each contributed exp2(0*sl2 - m) to l and 0 to O
+  // keys past the end were staged as zero rows: each contributed exp2(0 - m) to l (1 on the bounded path) and 0 to O
   l_run += __shfl_xor(l_run, 32, 64);  // the two lane halves hold the sums of complementary keys
   const int n_pad = nt > 0 ? max(0, t_end * KT - k_len) : 0;
   l_run -= (float)n_pad * __builtin_amdgcn_exp2f(-m_run);
@@ -786,6 +806,7 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
   q.n_main = (p.max_q + QT - 1) / QT;
   q.n_split = 0;
   const int pairs = p.B * p.H;
+  FLITE_REQUIRE(p.max_score <= kMaxBoundedScore, "attention: max_score above 40 (use 0, the online softmax)");
   FLITE_REQUIRE(p.part_mode == 0 || (p.max_score > 0.f && p.part_o && p.part_l),
                 "attention: partial (O, l) modes need the bounded softmax and both partial buffers");
   FLITE_REQUIRE(p.part_mode >= 0 && p.part_mode <= 3, "attention: part_mode is 0 (whole), 1 (write partial), "

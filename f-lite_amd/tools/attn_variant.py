@@ -19,7 +19,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 
 
-def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False):
+def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False, qlate=False):
     src = (HERE.parent / "csrc" / "attention.hip").read_text()
 
     def sub(old, new, count=1):
@@ -72,6 +72,19 @@ def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False):
             "      if constexpr (EX) l_run += e_prev;\n")
         sub("        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);\n",
             "        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);\n        l_run += e_prev;\n")
+    if qlate:  # Q^T moves to AGPRs (which waits for its loads) only AFTER the K_0 / V_0 / K_1 copies are issued,
+        # so the prologue pays max(Q latency, K/V latency) instead of their sum
+        pin = ("    if constexpr (BOUNDED) {  // move Q^T into AGPRs here, then clear the write -> MFMA-read hazard\n"
+               "#pragma unroll\n"
+               "      for (int s = 0; s < 16; ++s) asm volatile(\"\" : \"+a\"(qf[s]));\n"
+               "      asm volatile(\"s_nop 4\" ::: \"memory\");\n"
+               "    }\n")
+        sub(pin, "")
+        sub("        for (int i = 0; i < 8; ++i) blds16(krs, k_src[i], lds0 + TILE + (wave * 8 + i) * 1024 + K_OFF);\n"
+            "      }\n",
+            "        for (int i = 0; i < 8; ++i) blds16(krs, k_src[i], lds0 + TILE + (wave * 8 + i) * 1024 + K_OFF);\n"
+            "      }\n" + pin.replace("    if constexpr", "      if constexpr").replace("#pragma", "#pragma")
+            .replace("\n      for", "\n        for").replace("\n      asm", "\n        asm").replace("\n    }\n", "\n      }\n"))
     if vdma_b is not None:
         sub('''    auto phase_b = [&](auto vb_, auto ex_, u32x4 (&pc)[4], u32x4 (&pn)[4]) {
       constexpr int VB = decltype(vb_)::value;
@@ -111,4 +124,5 @@ if __name__ == "__main__":
     vb = None
     if "--vdma-b" in a:
         vb = int(a[a.index("--vdma-b") + 1])
-    make(name, kspread="--kspread" in a, vdma_b=vb, qscale="--qscale" in a, ldelay="--ldelay" in a)
+    make(name, kspread="--kspread" in a, vdma_b=vb, qscale="--qscale" in a, ldelay="--ldelay" in a,
+         qlate="--qlate" in a)

@@ -67,8 +67,9 @@ int flite_gemm_bf16_ws(void* stream, int M, int N, int K, const void* A, long ld
  * Replaces flash_attn_interface.flash_attn_varlen_func(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
  * max_seqlen_k, softmax_scale) (f_lite/model.py:203-210). Token t of sequence b is row cu[b]+t; head h of
  * a row starts at h*head_stride. cu_seqlens_* are device int32 [B+1]. Output o has the q layout.
- * max_score > 0 asserts |score*scale| <= max_score (QK-normed q, k): fixed-shift softmax, no online rescale;
- * max_score = 0 runs the general online softmax.
+ * max_score > 0 asserts |score*scale| <= max_score (QK-normed q, k): unshifted softmax p = exp2(score*scale*log2 e),
+ * no running max, no online rescale (max_score <= 40, so every sum stays in fp32 range); max_score = 0 runs the
+ * general online softmax.
  */
 int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void* v, void* o, long q_row_stride,
                           long k_row_stride, long v_row_stride, long o_row_stride, long head_stride,
