@@ -19,7 +19,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 
 
-def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False, qlate=False):
+def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False, qlate=False, packdelay=False):
     src = (HERE.parent / "csrc" / "attention.hip").read_text()
 
     def sub(old, new, count=1):
@@ -85,6 +85,32 @@ def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False, qlate=Fal
             "        for (int i = 0; i < 8; ++i) blds16(krs, k_src[i], lds0 + TILE + (wave * 8 + i) * 1024 + K_OFF);\n"
             "      }\n" + pin.replace("    if constexpr", "      if constexpr").replace("#pragma", "#pragma")
             .replace("\n      for", "\n        for").replace("\n      asm", "\n        asm").replace("\n    }\n", "\n      }\n"))
+    if packdelay:  # (product source: delayed row sum already in) the bf16 pair of scores (e-2, e-1) is packed at
+        # element e, so the v_cvt_pk never waits on the v_exp just issued; the last pair after the loop
+        sub("""      l_run += e_prev;
+      if (e & 1) {
+        const bf16x2 pr = {(__bf16)e_prev, (__bf16)v};
+        pn[(e >> 4) * 2 + (r >> 3)][(r & 7) >> 1] = __builtin_bit_cast(unsigned, pr);
+      }
+      e_prev = v;
+    };""", """      l_run += e_prev;
+      if (!(e & 1) && e >= 2) pack_pair(pn, e - 2, e_prev2, e_prev);
+      e_prev2 = e_prev;
+      e_prev = v;
+    };""")
+        sub("    auto softmax_elem = [&](u32x4 (&pn)[4], int e, float& e_prev) {",
+            """    auto pack_pair = [&](u32x4 (&pn)[4], int e, float a, float b) {  // scores e, e + 1 (e even)
+      const int r = e & 15;
+      const bf16x2 pr = {(__bf16)a, (__bf16)b};
+      pn[(e >> 4) * 2 + (r >> 3)][(r & 7) >> 1] = __builtin_bit_cast(unsigned, pr);
+    };
+    float e_prev2 = 0.f;
+    auto softmax_elem = [&](u32x4 (&pn)[4], int e, float& e_prev) {""")
+        sub("      if constexpr (EX) l_run += e_prev;\n",
+            "      if constexpr (EX) {\n        l_run += e_prev;\n        pack_pair(pn, 30, e_prev2, e_prev);\n      }\n")
+        sub("        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);\n        l_run += e_prev;\n",
+            "        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);\n        l_run += e_prev;\n"
+            "        pack_pair(pa, 30, e_prev2, e_prev);\n")
     if vdma_b is not None:
         sub('''    auto phase_b = [&](auto vb_, auto ex_, u32x4 (&pc)[4], u32x4 (&pn)[4]) {
       constexpr int VB = decltype(vb_)::value;
@@ -125,4 +151,4 @@ if __name__ == "__main__":
     if "--vdma-b" in a:
         vb = int(a[a.index("--vdma-b") + 1])
     make(name, kspread="--kspread" in a, vdma_b=vb, qscale="--qscale" in a, ldelay="--ldelay" in a,
-         qlate="--qlate" in a)
+         qlate="--qlate" in a, packdelay="--packdelay" in a)
