@@ -447,7 +447,15 @@ def main():
     f_ref_image = args.sample_steps * 2 * f_step + 2 * f_once + f_vae
     dedup = args.mode == "replica" and args.guidance >= 1.0 and os.environ.get("FLITE_NO_CFG_DEDUP") is None
     f_dedup = args.sample_steps * (2 * T * D * 3 * D + 4 * T * T * D + 2 * T * D * D) if dedup else 0.0
-    f_image = f_ref_image - f_dedup
+    # uniform-context collapse (dit.cpp set_context): the uncond copy's context is the pipeline's zero negative prompt
+    # (pipeline.py:160-161), so its cross-attention keys/values are all equal and its cross-attention sub-block is
+    # the step-invariant x += gate * (V . Wproj^T): no cross-q GEMM, attention or cross-proj GEMM for those rows
+    cross_blocks = sum(1 for i in range(cfg["depth"]) if cfg["per_block_adaln"] or i % 4 == 0 or i < 8)
+    collapse = (args.mode != "sp" and args.mode != "sp-ring" and args.guidance >= 1.0 and not args.fp8
+                and os.environ.get("FLITE_NO_CTX_COLLAPSE") is None)
+    f_collapse = (args.sample_steps * cross_blocks * (2 * T * D * D + 4 * T * 512 * D + 2 * T * D * D)
+                  if collapse else 0.0)
+    f_image = f_ref_image - f_dedup - f_collapse
     M = 2 * BI * T
     per_launch = {
         "gateup": (2.0 * M * 2 * F * D, "SwiGLU gate/up GEMM (M=%d, N=%d, K=%d)" % (M, 2 * F, D)),
@@ -539,6 +547,7 @@ def main():
         "algorithmic_flops_per_image": f_image,
         "reference_flops_per_image": f_ref_image,
         "cfg_dedup_flops_per_image": f_dedup,
+        "uniform_ctx_collapse_flops_per_image": f_collapse,
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

@@ -43,6 +43,15 @@ bool norm_prefetch() {
   return on;
 }
 
+// Uniform-context collapse: a sequence whose context rows are all equal (the pipeline's zero negative prompt) has
+// equal cross-attention keys and values, so its cross-attention output is the V row for every query, and the whole
+// cross-attention sub-block reduces to x += gate_ca * (V . Wproj^T), step-invariant (set_context makes it once).
+// FLITE_NO_CTX_COLLAPSE=1 computes those rows like any other (A/B switch and test reference).
+bool ctx_collapse() {
+  static const bool on = getenv("FLITE_NO_CTX_COLLAPSE") == nullptr;
+  return on;
+}
+
 bool parse_block(const std::string& name, int* idx, std::string* rest) {
   if (name.rfind("blocks.", 0) != 0) return false;
   const size_t dot = name.find('.', 7);
@@ -281,6 +290,10 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   }
   if (alloc((void**)&cu_self_, (B + 1) * 4)) return 1;
   if (alloc((void**)&cu_ctx_, (B + 1) * 4)) return 1;
+  if (alloc((void**)&ctx_c_, (long)cfg.depth * B * D * 4)) return 1;
+  if (alloc((void**)&ctx_vrow_, (long)B * D * 2)) return 1;
+  if (alloc((void**)&ctx_bad_, (long)B * 4)) return 1;
+  ctx_uni_ = 0;
   // RoPE tables for every row a rank may hold (the last rank's padding rows read zeros)
   if (alloc((void**)&cos_, (long)sp_n_ * Tl_ * 128 * 4)) return 1;
   if (alloc((void**)&sin_, (long)sp_n_ * Tl_ * 128 * 4)) return 1;
@@ -416,6 +429,36 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
     rn.heads = H;
     rn.rope_heads = 0;
     if (rope_qknorm(rn, s)) return 1;
+  }
+  // uniform-context collapse: the leading sequences whose rows are all equal, and their c = V . Wproj^T per block
+  int uni = 0;
+  if (ctx_collapse() && sp_n_ == 1) {
+    FLITE_HIP_CHECK(hipMemsetAsync(ctx_bad_, 0, (size_t)nseq * 4, s));
+    if (rows_uniform(ctx, cfg.cross_attn_input_size, cu_ctx_, nseq, ctx_bad_, s)) return 1;
+    std::vector<int> bad(nseq);
+    FLITE_HIP_CHECK(hipMemcpyAsync(bad.data(), ctx_bad_, (size_t)nseq * 4, hipMemcpyDeviceToHost, s));
+    FLITE_HIP_CHECK(hipStreamSynchronize(s));
+    while (uni < nseq && cu_host[uni + 1] > cu_host[uni] && !bad[uni]) ++uni;
+  }
+  if (uni != ctx_uni_) drop_graph();  // a cached graph holds the other launch shapes
+  ctx_uni_ = uni;
+  for (int i = 0; i < cfg.depth && uni > 0; ++i) {
+    const BlockW& b = w_.blocks[i];
+    if (!b.cross) continue;
+    for (int q = 0; q < uni; ++q)  // the sequence's V row (model.py:189-196: every key of it has this value)
+      FLITE_HIP_CHECK(hipMemcpyAsync(ctx_vrow_ + (long)q * D, ctx_kv_[i] + (long)cu_host[q] * 2 * D + D,
+                                     (size_t)D * 2, hipMemcpyDeviceToDevice, s));
+    GemmParams g;
+    g.A = ctx_vrow_;
+    g.lda = D;
+    g.W = b.cproj_w;
+    g.ldw = D;
+    g.out = ctx_c_ + (long)i * B_ * D;
+    g.ldo = D;
+    g.M = uni;
+    g.N = D;
+    g.K = D;
+    if (gemm(g, EPI_STORE_F32, s)) return 1;
   }
   ctx_stale_ = false;
   return 0;
@@ -620,30 +663,55 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     FLITE_HIP_CHECK(hipMemcpyAsync(x_ + r0 * D, x_, (size_t)Msa * D * sizeof(float), hipMemcpyDeviceToDevice, s));
 
   // --- cross attention (model.py:291-297) ---
-  if (b.cross) {
-    if (norm(b.norm2, shift_ca, scale_ca, b.cq_w, (long)D * D)) return 1;
+  // The first ctx_uni_ sequences have uniform context (set_context): their rows take the step-invariant
+  // x += gate_ca * c; the norm, the cross-q GEMM, the attention and the cross-proj run on the other rows only.
+  const int U = b.cross ? ctx_uni_ : 0;
+  const long r0 = (long)U * Tl_;
+  if (U > 0 && ctx_bcast_resid(x_, ctx_c_ + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s)) return 1;
+  if (b.cross && r0 < M_) {
+    {
+      NormModParams nm;
+      if (norm_prefetch()) {
+        nm.pf[0] = b.cq_w;
+        nm.pf_bytes[0] = (long)D * D * 2;
+      }
+      nm.x = x_ + r0 * D;
+      nm.ldx = D;
+      nm.y = nbuf_ + r0 * D;
+      nm.ldy = D;
+      nm.w = b.norm2;
+      nm.shift = shift_ca + U * mseg;
+      nm.scale = scale_ca + U * mseg;
+      nm.mod_seg_stride = mseg;
+      nm.rows = M_ - r0;
+      nm.D = D;
+      nm.in_seg = Tl_;
+      nm.in_stride = Tl_;
+      nm.in_off = 0;
+      if (rmsnorm_mod(nm, false, s)) return 1;
+    }
     GemmParams g;
-    g.A = nbuf_;
+    g.A = nbuf_ + r0 * D;
     g.lda = D;
     g.W = b.cq_w;
     g.ldw = D;
     g.bias = b.cq_b;
-    g.out = qkv_;
+    g.out = qkv_ + r0 * D;
     g.ldo = D;
     if (w_prefetch()) {  // the cross-proj weights, read after the cross-attention
       g.pf = b.cproj_w;
       g.pf_bytes = (long)D * D * 2;
     }
-    g.M = (int)M_;
+    g.M = (int)(M_ - r0);
     g.N = D;
     g.K = D;
     g.norm_cols = D;  // query QK-norm (model.py:197) in the epilogue
     if (gemm(g, fuse_qk_norm() ? EPI_QKV_NORM_BF16 : EPI_STORE_BF16, s)) return 1;
     if (!fuse_qk_norm()) {
       RopeNormParams rn;
-      rn.x = qkv_;
+      rn.x = qkv_ + r0 * D;
       rn.ldx = D;
-      rn.rows = M_;
+      rn.rows = M_ - r0;
       rn.heads = H;
       rn.rope_heads = 0;
       if (rope_qknorm(rn, s)) return 1;
@@ -657,9 +725,9 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.k_row_stride = a.v_row_stride = 2L * D;
     a.o_row_stride = D;
     a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = HEAD_DIM;
-    a.cu_q = cu_self_;
-    a.cu_k = cu_ctx_;
-    a.B = B_;
+    a.cu_q = cu_self_ + U;  // absolute row offsets: the collapsed sequences are skipped, nothing else moves
+    a.cu_k = cu_ctx_ + U;
+    a.B = B_ - U;
     a.H = H;
     a.head_dim = HEAD_DIM;
     a.max_q = Tl_;
@@ -669,7 +737,20 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     a.split_ws = attn_ws_;
     a.split_ws_bytes = attn_ws_bytes_;
     if (attn_fwd(a, s)) return 1;
-    if (resid(obuf_, D, b.cproj_w, D, gate_ca)) return 1;
+    GemmParams c;
+    c.A = obuf_ + r0 * D;
+    c.lda = D;
+    c.W = b.cproj_w;
+    c.ldw = D;
+    c.out = x_ + r0 * D;
+    c.ldo = D;
+    c.gate = gate_ca + U * mseg;
+    c.gate_seg_stride = mseg;
+    c.rows_per_seg = Tl_;
+    c.M = (int)(M_ - r0);
+    c.N = D;
+    c.K = D;
+    if (gemm(c, EPI_RESID_F32, s)) return 1;
   }
 
   // --- SwiGLU MLP (model.py:299-301) ---

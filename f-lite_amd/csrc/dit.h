@@ -118,6 +118,12 @@ class DitEngine {
   long M_ = 0;
   int sa_seqs_ = 0;  // > 0: block 0's self-attention on the first sa_seqs_ sequences only (forward, CFG batch)
   int nctx_ = 0, nseq_ctx_ = 0, ctx_max_len_ = 0;
+  // uniform-context collapse (set_context, run_block): the first ctx_uni_ sequences have context rows that are all
+  // equal (the pipeline's zero negative prompt, pipeline.py:160-161); ctx_c_[blk][seq] = V row . Wproj^T (fp32)
+  int ctx_uni_ = 0;
+  float* ctx_c_ = nullptr;
+  bf16_t* ctx_vrow_ = nullptr;
+  int* ctx_bad_ = nullptr;
   // workspace
   float* x_ = nullptr;
   bf16_t *nbuf_ = nullptr, *qkv_ = nullptr, *obuf_ = nullptr, *hbuf_ = nullptr, *patches_ = nullptr;

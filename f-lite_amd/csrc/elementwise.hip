@@ -429,6 +429,43 @@ __global__ __launch_bounds__(1024) void apg_euler_kernel(const float* out, float
 // the whole batch gets bit-identical sums.
 //   phase 0: out = [sum c (c - u), sum c^2]            (dy = c, dd = c - u: pipeline.py:278-281)
 //   phase 1: out = [sum o, sum o^2], o = (c - u) - k c  (orthogonal part, for its std: pipeline.py:282-284)
+// Uniform-context collapse (dit.cpp set_context / run_block). bad[s] = 1 when a row of context sequence s differs
+// (bit for bit) from its first row. Grid (nseq, chunks): chunk c compares rows first + 1 + c, + chunks, ...; a
+// mismatch is recorded by plain stores of 1 (any number of lanes may store it; the host zeroes bad first).
+__global__ __launch_bounds__(256) void rows_uniform_kernel(const unsigned* x, long ld_words, const int* cu,
+                                                           int cols_words, int* bad) {
+  const int s = blockIdx.x;
+  const int r0 = cu[s], r1 = cu[s + 1];
+  const unsigned* first = x + (long)r0 * ld_words;
+  int diff = 0;
+  for (long r = r0 + 1 + blockIdx.y; r < r1; r += gridDim.y) {
+    const unsigned* row = x + r * ld_words;
+    for (int c = threadIdx.x; c < cols_words; c += blockDim.x) diff |= row[c] != first[c];
+  }
+  if (diff) bad[s] = 1;
+}
+
+// Collapsed rows r < rows (sequences whose cross-attention keys are all equal): the attention output of every such
+// row is the sequence's one V row, so the gated residual of its cross-proj is the step-invariant c[seq] = V.Wproj^T
+// (made once per set_context): x[r][n] += gate[seq][n] * c[seq][n] -- the cross-proj epilogue's own expression.
+__global__ __launch_bounds__(256) void ctx_bcast_resid_kernel(float* x, const float* c, const float* gate,
+                                                              long gate_seg_stride, int rows_per_seg, long rows,
+                                                              int D) {
+  const int d4 = D / 4;
+  const long n4 = rows * d4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / d4;
+    const int n = (int)(i - r * d4) * 4;
+    const long seq = r / rows_per_seg;
+    f32x4 xv = *(const f32x4*)(x + r * D + n);
+    const f32x4 cv = *(const f32x4*)(c + seq * D + n);
+    const f32x4 gv = *(const f32x4*)(gate + seq * gate_seg_stride + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[j] += cv[j] * gv[j];
+    *(f32x4*)(x + r * D + n) = xv;
+  }
+}
+
 // Device-resident scalars (flite_apg_sums_dev / flite_apg_euler_dev): ws[0..1] = the phase-0 sums, ws[2..3] = the
 // phase-1 sums, each after any all-reduce between the ranks; k and the orthogonal scale are derived where they are
 // used, with apg_euler_kernel's fp32 expressions, so a multi-rank APG step needs no host round trip.
@@ -693,6 +730,24 @@ int cfg_euler_nchw(const float* u, const float* c, float* acc, long n, float g, 
 int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, float g, float thr, float dt,
               hipStream_t s) {
   hipLaunchKernelGGL(apg_euler_kernel, dim3(1), dim3(1024), 0, s, out, acc, Bi, C, H, W, P, g, thr, dt);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int rows_uniform(const void* x, int cols, const int* cu, int nseq, int* bad, hipStream_t s) {
+  FLITE_REQUIRE(cols % 2 == 0 && nseq > 0, "rows_uniform: bf16 rows of even width");
+  hipLaunchKernelGGL(rows_uniform_kernel, dim3(nseq, 32), dim3(256), 0, s, (const unsigned*)x, (long)cols / 2, cu,
+                     cols / 2, bad);
+  FLITE_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int ctx_bcast_resid(float* x, const float* c, const float* gate, long gate_seg_stride, int rows_per_seg, long rows,
+                    int D, hipStream_t s) {
+  if (rows <= 0) return 0;
+  FLITE_REQUIRE(D % 4 == 0, "ctx_bcast_resid: D must be a multiple of 4");
+  hipLaunchKernelGGL(ctx_bcast_resid_kernel, dim3(grid_for(rows * (D / 4))), dim3(256), 0, s, x, c, gate,
+                     gate_seg_stride, rows_per_seg, rows, D);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

@@ -159,6 +159,9 @@ int apg_sums(const float* u, const float* c, long n, float k, int phase, float* 
 int apg_update_nchw(const float* u, const float* c, float* acc, long n, float g, float k, float sc, float dt,
                     hipStream_t s);
 int apg_sums_dev(const float* u, const float* c, long n, int phase, float* ws4, hipStream_t s);
+int rows_uniform(const void* x, int cols, const int* cu, int nseq, int* bad, hipStream_t s);
+int ctx_bcast_resid(float* x, const float* c, const float* gate, long gate_seg_stride, int rows_per_seg, long rows,
+                    int D, hipStream_t s);
 int apg_update_nchw_dev(const float* u, const float* c, float* acc, long n, float g, float thr, long n_total,
                         const float* ws4, float dt, hipStream_t s);
 int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, float g, float thr, float dt,

@@ -272,3 +272,75 @@ def test_cfg_block0_dedup_matches_full_batch(tmp_path):
     p = psnr(dd["tiny.True"], ref)
     print(f"CFG dedup, tiny, 2 images: {p:.2f} dB vs the fp32 oracle")
     assert p >= 35.0
+
+
+_COLLAPSE_SCRIPT = """
+import sys, torch
+sys.path[:0] = [{pkg!r}, {root!r}]
+from f_lite import DiT, FLitePipeline
+from f_lite.model import PRESETS
+out = {{}}
+for name, cfg, hw in (("tiny", dict(PRESETS["tiny"]), 128), ("10b_d2", dict(PRESETS["10b"], depth=2), 256)):
+    m = DiT.random(seed=0, device="cuda", **cfg)
+    g = torch.Generator().manual_seed(6)
+    C = cfg["cross_attn_input_size"]
+    lat = torch.randn(2, 16, hw // 8, hw // 8, generator=g).bfloat16().cuda()
+    pos = torch.randn(2, 24, C, generator=g).bfloat16().cuda()
+    negs = {{"zero": torch.zeros_like(pos),                                   # the pipeline default
+             "const": torch.randn(2, 1, C, generator=g).bfloat16().cuda().expand(2, 24, C).contiguous(),
+             "random": torch.randn(2, 24, C, generator=g).bfloat16().cuda()}}  # not uniform: no collapse
+    for kind, neg in negs.items():
+        for graph in (False, True):
+            out[f"{{name}}.{{kind}}.{{graph}}"] = FLitePipeline(m)(prompt_embeds=pos, negative_prompt_embeds=neg,
+                latents=lat, height=hw, width=hw, num_inference_steps=4, guidance_scale=6.0, output_type="latent",
+                use_graph=graph).images.float().cpu()
+    x = torch.randn(2, 16, hw // 8, hw // 8, generator=g).bfloat16().cuda()
+    t = torch.tensor([0.7, 0.7]).bfloat16().cuda()
+    out[f"{{name}}.fwd"] = m(torch.cat([x[:1], x[:1]]), torch.cat([negs["zero"][:1], pos[:1]]), None, t,
+                             output_dtype=torch.float32).cpu()
+    out[f"{{name}}.lat"], out[f"{{name}}.pos"] = lat.float().cpu(), pos.float().cpu()
+torch.save(out, sys.argv[1])
+"""
+
+
+def test_uniform_context_collapse_matches_full_computation(tmp_path):
+    """dit.cpp uniform-context collapse: a CFG uncond sequence whose context rows are all equal (the pipeline's zero
+    negative prompt; also a constant non-zero row) has equal cross-attention keys and values, so its cross-attention
+    sub-block is x += gate * (V . Wproj^T), made once per set_context. Against FLITE_NO_CTX_COLLAPSE=1 (child
+    processes): >= 60 dB (the full path rounds P to bf16 against the fp32 row sum, so its output is V to within one
+    bf16 ulp; the collapse takes V exactly); a random negative context is not collapsed (bit-identical); the sampling
+    loop with the default zero negative vs the fp32 oracle's batched CFG loop >= 35 dB."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    script = tmp_path / "collapse.py"
+    script.write_text(_COLLAPSE_SCRIPT.format(pkg=str(root / "f-lite_amd"), root=str(root)))
+    outs = []
+    for i, extra in enumerate(({}, {"FLITE_NO_CTX_COLLAPSE": "1"})):
+        f = tmp_path / f"o{i}.pt"
+        r = subprocess.run([sys.executable, str(script), str(f)], env=dict(os.environ, **extra), capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(torch.load(f, weights_only=True))
+    col, full = outs
+    for name in ("tiny", "10b_d2"):
+        for kind in ("zero", "const", "random"):
+            assert torch.equal(col[f"{name}.{kind}.False"], col[f"{name}.{kind}.True"])  # graph == eager
+            p = psnr(col[f"{name}.{kind}.True"], full[f"{name}.{kind}.True"])
+            print(f"uniform-context collapse vs full computation, {name}, {kind} negative context: {p:.2f} dB")
+            if kind == "random":
+                assert torch.equal(col[f"{name}.{kind}.True"], full[f"{name}.{kind}.True"])
+            else:
+                assert p >= 60.0
+        p = psnr(col[f"{name}.fwd"], full[f"{name}.fwd"])
+        print(f"  forward with [zero, prompt] contexts: {p:.2f} dB")
+        assert p >= 60.0
+    ref = R.sample(R.RefDiT.random(R.PRESETS["tiny"], dtype=torch.float32), col["tiny.lat"], col["tiny.pos"],
+                   torch.zeros_like(col["tiny.pos"]), num_steps=4, guidance_scale=6.0, apg=R.APG(enabled=False),
+                   height=128, width=128, t_dtype=torch.bfloat16, acc_dtype=torch.float32)
+    p = psnr(col["tiny.zero.True"], ref)
+    print(f"collapse, tiny, zero negative: {p:.2f} dB vs the fp32 oracle")
+    assert p >= 35.0
