@@ -307,9 +307,12 @@ def test_uniform_context_collapse_matches_full_computation(tmp_path):
     """dit.cpp uniform-context collapse: a CFG uncond sequence whose context rows are all equal (the pipeline's zero
     negative prompt; also a constant non-zero row) has equal cross-attention keys and values, so its cross-attention
     sub-block is x += gate * (V . Wproj^T), made once per set_context. Against FLITE_NO_CTX_COLLAPSE=1 (child
-    processes): >= 60 dB (the full path rounds P to bf16 against the fp32 row sum, so its output is V to within one
-    bf16 ulp; the collapse takes V exactly); a random negative context is not collapsed (bit-identical); the sampling
-    loop with the default zero negative vs the fp32 oracle's batched CFG loop >= 35 dB."""
+    processes): >= 50 dB, and against the fp32 oracle's batched CFG loop the collapse is at least as close as the full
+    path (-0.3 dB slack) and >= 35 dB. The two paths are not bit-identical and need not be: the full path rounds P to
+    bf16 against the fp32 row sum, so its attention output is V only to within one bf16 ulp (measured 61.4 dB tiny,
+    57.1 dB 10b_d2 after 4 CFG-6 steps, which amplify the uncond branch 5x); the collapse takes V exactly. A random
+    negative context is not collapsed (bit-identical)."""
+    import dataclasses
     import os
     import subprocess
     import sys
@@ -334,13 +337,15 @@ def test_uniform_context_collapse_matches_full_computation(tmp_path):
             if kind == "random":
                 assert torch.equal(col[f"{name}.{kind}.True"], full[f"{name}.{kind}.True"])
             else:
-                assert p >= 60.0
+                assert p >= 50.0
         p = psnr(col[f"{name}.fwd"], full[f"{name}.fwd"])
         print(f"  forward with [zero, prompt] contexts: {p:.2f} dB")
         assert p >= 60.0
-    ref = R.sample(R.RefDiT.random(R.PRESETS["tiny"], dtype=torch.float32), col["tiny.lat"], col["tiny.pos"],
-                   torch.zeros_like(col["tiny.pos"]), num_steps=4, guidance_scale=6.0, apg=R.APG(enabled=False),
-                   height=128, width=128, t_dtype=torch.bfloat16, acc_dtype=torch.float32)
-    p = psnr(col["tiny.zero.True"], ref)
-    print(f"collapse, tiny, zero negative: {p:.2f} dB vs the fp32 oracle")
-    assert p >= 35.0
+    for name, cfg, hw in (("tiny", R.PRESETS["tiny"], 128), ("10b_d2", dataclasses.replace(R.PRESETS["10b"], depth=2),
+                                                             256)):
+        ref = R.sample(R.RefDiT.random(cfg, dtype=torch.float32), col[f"{name}.lat"], col[f"{name}.pos"],
+                       torch.zeros_like(col[f"{name}.pos"]), num_steps=4, guidance_scale=6.0, apg=R.APG(enabled=False),
+                       height=hw, width=hw, t_dtype=torch.bfloat16, acc_dtype=torch.float32)
+        pc, pf = psnr(col[f"{name}.zero.True"], ref), psnr(full[f"{name}.zero.True"], ref)
+        print(f"{name}, zero negative, vs the fp32 oracle: collapse {pc:.2f} dB, full computation {pf:.2f} dB")
+        assert pc >= 35.0 and pc >= pf - 0.3
