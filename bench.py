@@ -451,7 +451,8 @@ def main():
     # (pipeline.py:160-161), so its cross-attention keys/values are all equal and its cross-attention sub-block is
     # the step-invariant x += gate * (V . Wproj^T): no cross-q GEMM, attention or cross-proj GEMM for those rows
     cross_blocks = sum(1 for i in range(cfg["depth"]) if cfg["per_block_adaln"] or i % 4 == 0 or i < 8)
-    collapse = (args.mode != "sp" and args.mode != "sp-ring" and args.guidance >= 1.0 and not args.fp8
+    # (fp8 blocks: where the collapsed rows end on a 4-row boundary, dit.cpp uni_fp8)
+    collapse = (args.mode != "sp" and args.mode != "sp-ring" and args.guidance >= 1.0 and (not args.fp8 or T % 4 == 0)
                 and os.environ.get("FLITE_NO_CTX_COLLAPSE") is None)
     f_collapse = (args.sample_steps * cross_blocks * (2 * T * D * D + 4 * T * 512 * D + 2 * T * D * D)
                   if collapse else 0.0)

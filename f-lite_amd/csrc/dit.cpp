@@ -293,7 +293,11 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   if (alloc((void**)&ctx_c_, (long)cfg.depth * B * D * 4)) return 1;
   if (alloc((void**)&ctx_vrow_, (long)B * D * 2)) return 1;
   if (alloc((void**)&ctx_bad_, (long)B * 4)) return 1;
+  if (alloc((void**)&ctx_c8_, (long)cfg.depth * B * D * 4)) return 1;
+  if (alloc((void**)&ctx_vrow8_, (long)B * D)) return 1;
+  if (alloc((void**)&ctx_vrow8_s_, (long)(D / 128) * 256 * 4)) return 1;
   ctx_uni_ = 0;
+  ctx_c8_stale_ = true;
   // RoPE tables for every row a rank may hold (the last rank's padding rows read zeros)
   if (alloc((void**)&cos_, (long)sp_n_ * Tl_ * 128 * 4)) return 1;
   if (alloc((void**)&sin_, (long)sp_n_ * Tl_ * 128 * 4)) return 1;
@@ -442,6 +446,8 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
   }
   if (uni != ctx_uni_) drop_graph();  // a cached graph holds the other launch shapes
   ctx_uni_ = uni;
+  ctx_row0_.assign(cu_host, cu_host + uni);
+  ctx_c8_stale_ = true;
   for (int i = 0; i < cfg.depth && uni > 0; ++i) {
     const BlockW& b = w_.blocks[i];
     if (!b.cross) continue;
@@ -779,7 +785,9 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
 
 int DitEngine::alloc_fp8_act() {
   if (nbuf8_ != nullptr || x_ == nullptr) return 0;
-  mpad_ = mx_rows_pad(M_);
+  // + 256: a GEMM over rows [r0, M) (the uniform-context collapse, run_block_fp8) stages 256-row tiles of scales
+  // from row r0 on, i.e. up to row r0 + mx_rows_pad(M - r0) <= M + 255
+  mpad_ = mx_rows_pad(M_) + 256;
   const size_t sd = (size_t)(D / 128) * mpad_ * 4, sf = (size_t)(F / 128) * mpad_ * 4;
   if (alloc((void**)&nbuf8_, (size_t)M_ * D)) return 1;
   if (alloc((void**)&obuf8_, (size_t)M_ * D)) return 1;
@@ -866,6 +874,46 @@ int DitEngine::quantise_fp8(hipStream_t s) {
   }
   FLITE_HIP_CHECK(hipStreamSynchronize(s));
   w8_stale_ = false;
+  ctx_c8_stale_ = true;
+  return 0;
+}
+
+// The fp8 blocks' collapsed cross-attention rows need the collapsed-row offset r0 = U * Tl to keep the MXFP8 scale
+// arrays 16-B aligned (gemm_fp8: scales + r0 * 4 bytes); otherwise those blocks run the full computation.
+int DitEngine::uni_fp8() const { return ((long)ctx_uni_ * Tl_) % 4 == 0 ? ctx_uni_ : 0; }
+
+// c8[blk][q] = MX(V row) . MX(Wproj)^T: the fp8 path's own cross-proj arithmetic on the attention output the
+// collapse replaces (run_block_fp8). Runs before forward / sample launch any block, never inside a capture.
+int DitEngine::collapse_fp8(hipStream_t s) {
+  if (!ctx_c8_stale_) return 0;
+  const int U = uni_fp8();
+  for (int i = 0; i < cfg.depth && U > 0; ++i) {
+    const BlockW& b = w_.blocks[i];
+    if (!b.cross) continue;
+    for (int q = 0; q < U; ++q)
+      FLITE_HIP_CHECK(hipMemcpyAsync(ctx_vrow_ + (long)q * D, ctx_kv_[i] + (long)ctx_row0_[q] * 2 * D + D,
+                                     (size_t)D * 2, hipMemcpyDeviceToDevice, s));
+    if (quant_rows_fp8(ctx_vrow_, D, U, D, ctx_vrow8_, D, ctx_vrow8_s_, 256, s)) return 1;
+    float* c8 = ctx_c8_ + (long)i * B_ * D;
+    FLITE_HIP_CHECK(hipMemsetAsync(c8, 0, (size_t)U * D * 4, s));
+    GemmFp8Params g;
+    g.A = ctx_vrow8_;
+    g.lda = D;
+    g.As = ctx_vrow8_s_;
+    g.a_rows_pad = 256;
+    g.W = w8_[i].cproj;
+    g.ldw = D;
+    g.Ws = w8_[i].cproj_s;
+    g.w_rows_pad = D;
+    g.out = c8;
+    g.ldo = D;
+    g.rows_per_seg = 1;  // no gate: c8 += acc
+    g.M = U;
+    g.N = D;
+    g.K = D;
+    if (gemm_fp8(g, EPI8_RESID_F32, s)) return 1;
+  }
+  ctx_c8_stale_ = false;
   return 0;
 }
 
@@ -880,19 +928,19 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   const int Bsa = sa_seqs_ > 0 ? sa_seqs_ : B_;  // as run_block: block 0 of a CFG batch, self-attention once
   const long Msa = (long)Bsa * Tl_;
   const bool probe_sa = Msa == M_;
-  auto norm8 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0) -> int {
-    NormModParams nm;
-    nm.x = x_;
+  auto norm8 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0, long r0 = 0) -> int {
+    NormModParams nm;  // rows [r0, r0 + rows) of x; r0 % 4 == 0 keeps the scale rows 16-B aligned (uni_fp8)
+    nm.x = x_ + r0 * D;
     nm.ldx = D;
-    nm.y8 = nbuf8_;
+    nm.y8 = nbuf8_ + r0 * D;
     nm.ldy = D;
-    nm.ysc = nbuf8_s_;
+    nm.ysc = nbuf8_s_ + r0 * 4;
     nm.ysc_rows_pad = mpad_;
     nm.w = w;
     nm.shift = sh;
     nm.scale = sc;
     nm.mod_seg_stride = mseg;
-    nm.rows = rows > 0 ? rows : M_;
+    nm.rows = rows > 0 ? rows : M_ - r0;
     nm.D = D;
     nm.in_seg = Tl_;
     nm.in_stride = Tl_;
@@ -935,7 +983,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     return gemm_fp8(g, epi, s);
   };
   auto attn = [&](const bf16_t* qp, long ldq, const bf16_t* kp, const bf16_t* vp, long ldkv, const int* cu_k,
-                  int max_k, int nseq = 0) -> int {
+                  int max_k, int nseq = 0, int seq0 = 0) -> int {
     AttnParams a;
     a.q = qp;
     a.k = kp;
@@ -945,7 +993,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     a.k_row_stride = a.v_row_stride = ldkv;
     a.o_row_stride = D;
     a.q_head_stride = a.k_head_stride = a.v_head_stride = a.o_head_stride = HEAD_DIM;
-    a.cu_q = cu_self_;
+    a.cu_q = cu_self_ + seq0;
     a.cu_k = cu_k;
     a.B = nseq > 0 ? nseq : B_;
     a.H = H;
@@ -963,9 +1011,9 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     }
     return attn_fwd(a, s);
   };
-  auto qk_norm = [&](long ldx, int heads, int rope_heads, long rows = 0) -> int {
+  auto qk_norm = [&](long ldx, int heads, int rope_heads, long rows = 0, long r0 = 0) -> int {
     RopeNormParams rn;
-    rn.x = qkv_;
+    rn.x = qkv_ + r0 * ldx;
     rn.ldx = ldx;
     rn.rows = rows > 0 ? rows : M_;
     rn.heads = heads;
@@ -993,16 +1041,23 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa, 0, 0, Msa)) return 1;
   for (long r0 = Msa; r0 < M_; r0 += Msa)  // the other CFG copies of the residual rows
     FLITE_HIP_CHECK(hipMemcpyAsync(x_ + r0 * D, x_, (size_t)Msa * D * sizeof(float), hipMemcpyDeviceToDevice, s));
-  // --- cross attention ---
-  if (b.cross) {
-    if (norm8(b.norm2, shift_ca, scale_ca)) return 1;
-    if (g8(nbuf8_, nbuf8_s_, q.cq, q.cq_s, D, D, D, b.cq_b, fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16, qkv_, D,
-           nullptr, D, 0))
+  // --- cross attention --- (uniform-context collapse as in run_block: the first U sequences' rows take
+  // x += gate_ca * c8, the rest run the sub-block from row r0 on)
+  const int U = b.cross ? uni_fp8() : 0;
+  const long r0 = (long)U * Tl_, rows = M_ - r0;
+  if (U > 0 && ctx_bcast_resid(x_, ctx_c8_ + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s)) return 1;
+  if (b.cross && rows > 0) {
+    if (norm8(b.norm2, shift_ca + U * mseg, scale_ca + U * mseg, rows, r0)) return 1;
+    if (g8(nbuf8_ + r0 * D, nbuf8_s_ + r0 * 4, q.cq, q.cq_s, D, D, D, b.cq_b,
+           fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16, qkv_ + r0 * D, D, nullptr, D, 0, rows))
       return 1;
-    if (!fused && qk_norm(D, H, 0)) return 1;
-    if (attn(qkv_, D, ctx_kv_[blk], ctx_kv_[blk] + D, 2L * D, cu_ctx_, ctx_max_len_)) return 1;
-    if (!attn_mx_ && quant_rows_fp8(obuf_, D, M_, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
-    if (g8(obuf8_, obuf8_s_, q.cproj, q.cproj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_ca)) return 1;
+    if (!fused && qk_norm(D, H, 0, rows, r0)) return 1;
+    if (attn(qkv_, D, ctx_kv_[blk], ctx_kv_[blk] + D, 2L * D, cu_ctx_ + U, ctx_max_len_, B_ - U, U)) return 1;
+    if (!attn_mx_ && quant_rows_fp8(obuf_ + r0 * D, D, rows, D, obuf8_ + r0 * D, D, obuf8_s_ + r0 * 4, mpad_, s))
+      return 1;
+    if (g8(obuf8_ + r0 * D, obuf8_s_ + r0 * 4, q.cproj, q.cproj_s, D, D, D, nullptr, EPI8_RESID_F32, x_ + r0 * D, D,
+           gate_ca + U * mseg, 0, 0, rows))
+      return 1;
   }
   // --- SwiGLU MLP ---
   if (norm8(b.norm3, shift_mlp, scale_mlp)) return 1;
@@ -1061,6 +1116,7 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
   FLITE_REQUIRE(sp_n_ == 1 || (sp_kv_send_ && sp_kv_recv_ && sp_out_send_ && sp_out_recv_),
                 "forward: sequence parallelism needs its exchange buffers (flite_dit_sp_bind_buffers)");
   if (fp8_ && w8_stale_ && quantise_fp8(s)) return 1;  // a weight was rebound since the fp8 copies were made
+  if (fp8_ && collapse_fp8(s)) return 1;
   const int cpp = C * P * P;
   // patch embed (model.py:533) straight into the residual stream after the registers (model.py:535)
   if (patchify(lat, lat_bf16, patches_, Bi, C, Hl_, Wl_, P, dup, s)) return 1;
@@ -1342,6 +1398,7 @@ int DitEngine::sample(hipStream_t s, float* acc, int Bi, int n_steps, const floa
   FLITE_REQUIRE(!ctx_stale_, "sample: context K/V cache is stale (weights changed since set_context, or it "
                 "failed): set the context again");
   if (fp8_ && w8_stale_ && quantise_fp8(s)) return 1;  // before any capture: quantise_fp8 synchronises
+  if (fp8_ && collapse_fp8(s)) return 1;
   // timesteps: one row per step, shared by every sample of the batch (pipeline.py:260,268)
   FLITE_HIP_CHECK(hipMemcpyAsync(tdev_, t_host, n_steps * 4, hipMemcpyHostToDevice, s));
   if (set_timesteps(s, tdev_, n_steps, cfg.bf16_timestep_quant)) return 1;

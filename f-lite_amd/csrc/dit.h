@@ -124,6 +124,14 @@ class DitEngine {
   float* ctx_c_ = nullptr;
   bf16_t* ctx_vrow_ = nullptr;
   int* ctx_bad_ = nullptr;
+  std::vector<int> ctx_row0_;  // first context row of each collapsed sequence (its V row in ctx_kv_)
+  // fp8 blocks: the same c from the MXFP8 V row and cross-proj weights (collapse_fp8, before the first fp8 use after
+  // set_context or a requantisation); only where the collapsed rows end on a 4-row boundary (uni_fp8)
+  float* ctx_c8_ = nullptr;
+  uint8_t *ctx_vrow8_ = nullptr, *ctx_vrow8_s_ = nullptr;
+  bool ctx_c8_stale_ = true;
+  int collapse_fp8(hipStream_t s);
+  int uni_fp8() const;
   // workspace
   float* x_ = nullptr;
   bf16_t *nbuf_ = nullptr, *qkv_ = nullptr, *obuf_ = nullptr, *hbuf_ = nullptr, *patches_ = nullptr;

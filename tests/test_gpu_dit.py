@@ -280,8 +280,13 @@ sys.path[:0] = [{pkg!r}, {root!r}]
 from f_lite import DiT, FLitePipeline
 from f_lite.model import PRESETS
 out = {{}}
-for name, cfg, hw in (("tiny", dict(PRESETS["tiny"]), 128), ("10b_d2", dict(PRESETS["10b"], depth=2), 256)):
+for name, cfg, hw, fp8 in (("tiny", dict(PRESETS["tiny"]), 128, None),
+                           ("10b_d2", dict(PRESETS["10b"], depth=2), 256, None),
+                           ("10b_d2_fp8", dict(PRESETS["10b"], depth=2), 256, ()),      # MXFP8, every block
+                           ("10b_d2_fp8mix", dict(PRESETS["10b"], depth=2), 256, (0,))):  # block 0 bf16
     m = DiT.random(seed=0, device="cuda", **cfg)
+    if fp8 is not None:
+        m.enable_fp8(True, bf16_blocks=fp8)
     g = torch.Generator().manual_seed(6)
     C = cfg["cross_attn_input_size"]
     lat = torch.randn(2, 16, hw // 8, hw // 8, generator=g).bfloat16().cuda()
@@ -311,7 +316,10 @@ def test_uniform_context_collapse_matches_full_computation(tmp_path):
     path (-0.3 dB slack) and >= 35 dB. The two paths are not bit-identical and need not be: the full path rounds P to
     bf16 against the fp32 row sum, so its attention output is V only to within one bf16 ulp (measured 61.4 dB tiny,
     57.1 dB 10b_d2 after 4 CFG-6 steps, which amplify the uncond branch 5x); the collapse takes V exactly. A random
-    negative context is not collapsed (bit-identical)."""
+    negative context is not collapsed (bit-identical). MXFP8 (all blocks, and block 0 bf16 + block 1 fp8): the
+    collapse quantises V where the full path quantises the attention output (V to within a bf16 ulp), which moves an
+    occasional e4m3 rounding: >= 30 dB between the two, and against the bf16 full computation the collapse is at least
+    as close as the full fp8 path (-0.5 dB slack)."""
     import dataclasses
     import os
     import subprocess
@@ -329,7 +337,8 @@ def test_uniform_context_collapse_matches_full_computation(tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(torch.load(f, weights_only=True))
     col, full = outs
-    for name in ("tiny", "10b_d2"):
+    for name in ("tiny", "10b_d2", "10b_d2_fp8", "10b_d2_fp8mix"):
+        fp8 = "fp8" in name
         for kind in ("zero", "const", "random"):
             assert torch.equal(col[f"{name}.{kind}.False"], col[f"{name}.{kind}.True"])  # graph == eager
             p = psnr(col[f"{name}.{kind}.True"], full[f"{name}.{kind}.True"])
@@ -337,10 +346,15 @@ def test_uniform_context_collapse_matches_full_computation(tmp_path):
             if kind == "random":
                 assert torch.equal(col[f"{name}.{kind}.True"], full[f"{name}.{kind}.True"])
             else:
-                assert p >= 50.0
+                assert p >= (30.0 if fp8 else 50.0)
+            if fp8 and kind != "random":
+                bf = full[f"10b_d2.{kind}.True"]
+                pc, pf = psnr(col[f"{name}.{kind}.True"], bf), psnr(full[f"{name}.{kind}.True"], bf)
+                print(f"  vs the bf16 full computation: collapse {pc:.2f} dB, full fp8 computation {pf:.2f} dB")
+                assert pc >= pf - 0.5
         p = psnr(col[f"{name}.fwd"], full[f"{name}.fwd"])
         print(f"  forward with [zero, prompt] contexts: {p:.2f} dB")
-        assert p >= 60.0
+        assert p >= (35.0 if fp8 else 60.0)
     for name, cfg, hw in (("tiny", R.PRESETS["tiny"], 128), ("10b_d2", dataclasses.replace(R.PRESETS["10b"], depth=2),
                                                              256)):
         ref = R.sample(R.RefDiT.random(cfg, dtype=torch.float32), col[f"{name}.lat"], col[f"{name}.pos"],
