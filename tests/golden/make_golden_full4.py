@@ -2,7 +2,7 @@
 
 Run in the build container only (needs /root/reference; ~6-8 h of CPU, ~40 GB of RAM; resumable):
 
-    python tests/golden/make_golden_full4.py [--threads 6] [--only KEY ...]
+    python tests/golden/make_golden_full4.py [--threads 6] [--only KEY ...] [--no-image]
 
 Same stub-loading and block streaming as make_golden_full.py (the reference's own DiT.forward, DiTBlock.forward
 and FLitePipeline.__call__; the 10B-v2 top level is make_golden.v2_forward_fixed), at the metric's
@@ -16,10 +16,13 @@ Fixtures (tests/golden/golden_full4.safetensors) + golden_full4_meta.json:
                                + shift (pipeline.py:304), i.e. exactly what reaches vae.decode
   10b.1024.s30.g6.bf16.final   the same run in the reference's bf16 arithmetic (its own floor vs fp32)
   10b.1024.s30.g1.f32.final    CFG 1 (pipeline.py:248: guidance >= 1 still runs the CFG batch), fp32
+  7b.1024.s30.g1.f32.final     BASELINE configs[1]'s model (7B, model.py layout) at CFG 1, fp32 (when time allows)
   10b.1024.s30.g1.bf16.final   CFG 1, bf16 (when time allows)
+  7b.1024.s30.g6.f32.final     7B at CFG 6, fp32 (when time allows)
   {key}.image                  uint8 [1, 1024, 1024, 3]: oracle/vae_ref.py (the restated Flux decoder, seed-0
                                generator weights) on that trajectory's final latents + pipeline.py:324-326; the
-                               bf16 runs' images give the reference's own image-space floor (meta *.image_bf16_vs_f32)
+                               bf16 runs' images give the reference's own image-space floor (meta *.image_bf16_vs_f32).
+                               Made right after each trajectory (and first, for finals that lack one).
 
 CFG 1 shortcut (stated): at guidance 1 pipeline.py:290 forms uncond + 1 * (cond - uncond). The wrapper below runs
 the reference DiT on the cond half only and hands the pipeline [cond, cond], so the combination returns cond
@@ -56,11 +59,14 @@ STEPS = 30
 OUT = HERE / "golden_full4.safetensors"
 META = HERE / "golden_full4_meta.json"
 CACHE = REPO / ".golden_cache" / "full4"
-# (key, guidance, dtype, cond_only), in priority order: the >= 40 dB bar first, then the CFG-6 pair
+# (key, guidance, dtype, cond_only), in priority order: the >= 40 dB bar first, then the CFG-6 pair, then 7B
+# (model.py layout, BASELINE configs[1]) and the CFG-1 floor; the model is the key's first field
 TRAJ = [("10b.1024.s30.g1.f32", 1.0, torch.float32, True),
         ("10b.1024.s30.g6.f32", 6.0, torch.float32, False),
         ("10b.1024.s30.g6.bf16", 6.0, torch.bfloat16, False),
-        ("10b.1024.s30.g1.bf16", 1.0, torch.bfloat16, True)]
+        ("7b.1024.s30.g1.f32", 1.0, torch.float32, True),
+        ("10b.1024.s30.g1.bf16", 1.0, torch.bfloat16, True),
+        ("7b.1024.s30.g6.f32", 6.0, torch.float32, False)]
 
 
 def _digest(*ts):
@@ -132,10 +138,10 @@ def main():
                               "(bf16-rounded) under the names below",
                  "inputs": {"ctx": [MGF.CTX_NAME, [1, 512, 4096]],
                             "latents_1024": [MGF.LAT1024_NAME, [1, 16, 128, 128]]},
-                 "reference": "/root/reference f_lite/model_v2.py, pipeline.py (blocks streamed)",
-                 "steps": STEPS, "size": [1024, 1024], "model": "10b (model_v2 layout)",
+                 "reference": "/root/reference f_lite/model.py (7b), model_v2.py (10b), pipeline.py (blocks streamed)",
+                 "steps": STEPS, "size": [1024, 1024], "model": "key prefix: 10b (model_v2 layout), 7b (model.py)",
                  "cfg1": "cond half only, see make_golden_full4.py header",
-                 "vae_image": "oracle/vae_ref.py seed-0 weights on the fp32 final latents, uint8 NHWC"})
+                 "vae_image": "oracle/vae_ref.py seed-0 weights on each trajectory's final latents, uint8 NHWC"})
 
     def save():
         meta["shapes"] = {k: list(v.shape) for k, v in T.items()}
@@ -143,30 +149,9 @@ def main():
         META.write_text(json.dumps(meta, indent=1))
         log(f"wrote {len(T)} tensors to {OUT.name}")
 
-    todo = [tr for tr in TRAJ if (args.only is None or tr[0] in args.only) and f"{tr[0]}.final" not in T]
-    if todo:
-        MG.install_stubs()
-        model_v2 = MG.load_ref("model_v2")
-        pipeline = MG.load_ref("pipeline")
-        pos = MGF.hashed(MGF.CTX_NAME, (1, 512, 4096))
-        neg = torch.zeros_like(pos)
-        lat = MGF.hashed(MGF.LAT1024_NAME, (1, 16, 128, 128))
-        with torch.no_grad():
-            log("10b: generating weights")
-            dit, set_dtype = MGF.stream_dit(model_v2, MGF.CFG_7B, True, log)
-            fwd = V2Adapter(dit, model_v2)
-            for key, g, dt, cond_only in todo:
-                log(f"{key}: trajectory")
-                set_dtype(dt)
-                call = CachedCall(fwd, CACHE / key, cond_only, log)
-                T[f"{key}.final"] = MGF.run_pipe(pipeline, call, lat.to(dt), pos.to(dt), neg.to(dt), STEPS, g,
-                                                 1024, 1024).float()
-                base = key.rsplit(".", 1)[0]
-                if f"{base}.f32.final" in T and f"{base}.bf16.final" in T:
-                    meta[f"{base}.bf16_vs_f32_psnr"] = MGF.psnr(T[f"{base}.bf16.final"], T[f"{base}.f32.final"])
-                    log(f"  {base} reference bf16 vs fp32 final latents: {meta[f'{base}.bf16_vs_f32_psnr']:.2f} dB")
-                save()
-    if not args.no_image:
+    def images():
+        if args.no_image:
+            return
         for key, _, dt, _ in TRAJ:
             if f"{key}.final" in T and f"{key}.image" not in T:
                 log(f"{key}: oracle VAE decode")
@@ -180,6 +165,39 @@ def main():
                                                                                         1e-12))
                 log(f"  {base} reference bf16 vs fp32 image: {meta[f'{base}.image_bf16_vs_f32_psnr']:.2f} dB")
         save()
+
+    images()
+    todo = [tr for tr in TRAJ if (args.only is None or tr[0] in args.only) and f"{tr[0]}.final" not in T]
+    if todo:
+        MG.install_stubs()
+        mods = {"7b": (MG.load_ref("model"), False), "10b": (MG.load_ref("model_v2"), True)}
+        model_v2 = mods["10b"][0]
+        pipeline = MG.load_ref("pipeline")
+        pos = MGF.hashed(MGF.CTX_NAME, (1, 512, 4096))
+        neg = torch.zeros_like(pos)
+        lat = MGF.hashed(MGF.LAT1024_NAME, (1, 16, 128, 128))
+        loaded, fwd, set_dtype = None, None, None
+        with torch.no_grad():
+            for key, g, dt, cond_only in todo:
+                name = key.split(".")[0]
+                if name != loaded:  # one model's streamed weights at a time (~40 GB)
+                    fwd = set_dtype = dit = None
+                    log(f"{name}: generating weights")
+                    mod, per_block = mods[name]
+                    dit, set_dtype = MGF.stream_dit(mod, MGF.CFG_7B, per_block, log)
+                    fwd = V2Adapter(dit, model_v2) if per_block else dit
+                    loaded = name
+                log(f"{key}: trajectory")
+                set_dtype(dt)
+                call = CachedCall(fwd, CACHE / key, cond_only, log)
+                T[f"{key}.final"] = MGF.run_pipe(pipeline, call, lat.to(dt), pos.to(dt), neg.to(dt), STEPS, g,
+                                                 1024, 1024).float()
+                base = key.rsplit(".", 1)[0]
+                if f"{base}.f32.final" in T and f"{base}.bf16.final" in T:
+                    meta[f"{base}.bf16_vs_f32_psnr"] = MGF.psnr(T[f"{base}.bf16.final"], T[f"{base}.f32.final"])
+                    log(f"  {base} reference bf16 vs fp32 final latents: {meta[f'{base}.bf16_vs_f32_psnr']:.2f} dB")
+                save()
+                images()
 
 
 if __name__ == "__main__":

@@ -276,27 +276,28 @@ def gold4():
     return load_file(str(f)), json.loads((GOLD / "golden_full4_meta.json").read_text())
 
 
-@pytest.mark.parametrize("g", [6.0, 1.0])
-def test_10b_1024_30_steps_vs_reference(gold4, m10b, g):
+@pytest.mark.parametrize("name,g", [("10b", 6.0), ("10b", 1.0), ("7b", 1.0), ("7b", 6.0)])
+def test_10b_1024_30_steps_vs_reference(gold4, m7b, m10b, name, g):
     """BASELINE's metric workload end to end against the reference itself: 10B (model_v2 layout), 1024^2, 30 steps,
-    the hipGraph-captured loop the bench times. P3 final latents vs the reference's fp32 trajectory, beside (and
-    above) the reference's own bf16 run; at CFG 1 the SURVEY §8d bar of 40 dB. Then the uint8 image of the product
-    path (HIP loop + HIP VAE) vs oracle/vae_ref.py's decode of the reference's fp32 latents (peak 255): >= 40 dB at
-    CFG 1; at CFG 6 at least the reference's own bf16 run's image (decoded the same way)."""
+    the hipGraph-captured loop the bench times (and configs[1]'s 7B, model.py layout, where the fixture holds it).
+    P3 final latents vs the reference's fp32 trajectory, beside (and above) the reference's own bf16 run; at CFG 1
+    the SURVEY §8d bar of 40 dB. Then the uint8 image of the product path (HIP loop + HIP VAE) vs oracle/vae_ref.py's
+    decode of the reference's fp32 latents (peak 255): >= 40 dB at CFG 1; at CFG 6 at least the reference's own
+    bf16 run's image (decoded the same way)."""
     from f_lite.vae import AutoencoderKL
 
     gd, meta = gold4
-    key = f"10b.1024.s30.g{g:g}"
+    key = f"{name}.1024.s30.g{g:g}"
     if f"{key}.f32.final" not in gd:
         pytest.skip(f"{key} not in the fixture file yet")
-    pipe = FLitePipeline(m10b, vae=AutoencoderKL.random(seed=0))
+    pipe = FLitePipeline(m7b if name == "7b" else m10b, vae=AutoencoderKL.random(seed=0))
     assert (pipe.vae.config.scaling_factor, pipe.vae.config.shift_factor) == (SCALING, SHIFT)
     kw = dict(prompt_embeds=hashed(meta, "ctx"), latents=hashed(meta, "latents_1024"), height=1024, width=1024,
               num_inference_steps=30, guidance_scale=g, use_graph=True)
     lat = pipe(**kw, output_type="latent").images.float()
     p = psnr(lat / SCALING + SHIFT, gd[f"{key}.f32.final"])
     floor = meta.get(f"{key}.bf16_vs_f32_psnr")
-    print(f"10B 1024^2 30-step CFG-{g:g} final latents: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
+    print(f"{name} 1024^2 30-step CFG-{g:g} final latents: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
           f"{'n/a' if floor is None else f'{floor:.2f} dB'})")
     if floor is not None:
         assert p >= floor
