@@ -218,7 +218,11 @@ int flite_dit_bind(flite_dit* dit, const char* name, const void* ptr, long numel
  * n_t timestep rows. Re-entrant: a call with an equal/smaller shape is a no-op. */
 int flite_dit_prepare(flite_dit* dit, int batch, int latent_h, int latent_w, int n_ctx, int n_t);
 /* Context embeddings [cu[batch], cross_attn_input_size] bf16, packed by host cu_seqlens [batch+1]:
- * context_proj + context_norm + per-block cross-attention K/V (step-invariant cache). */
+ * context_proj + context_norm + per-block cross-attention K/V (step-invariant cache). Also finds the leading
+ * sequences whose context rows are all bit-identical (the pipeline's zero negative prompt, pipeline.py:160-161) and
+ * makes their step-invariant cross-attention output per block (the uniform-context collapse; env
+ * FLITE_NO_CTX_COLLAPSE=1 disables it). That test reads one int per sequence back to the host, so this call
+ * synchronises `stream` and is not graph-capturable (forward / sample are). */
 int flite_dit_set_context(flite_dit* dit, void* stream, const void* ctx, const int* cu_seqlens_host, int batch);
 /* Timesteps (device fp32 [n]): time embedding + adaLN/final modulation rows. quantize=1: the timesteps
  * tensor is bf16 in the reference call, so t and t*1000 are rounded to bf16 (pipeline.py:260, model.py:551). */
