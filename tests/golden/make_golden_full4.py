@@ -17,8 +17,8 @@ Fixtures (tests/golden/golden_full4.safetensors) + golden_full4_meta.json:
   10b.1024.s30.g6.bf16.final   the same run in the reference's bf16 arithmetic (its own floor vs fp32)
   10b.1024.s30.g1.f32.final    CFG 1 (pipeline.py:248: guidance >= 1 still runs the CFG batch), fp32
   7b.1024.s30.g1.f32.final     BASELINE configs[1]'s model (7B, model.py layout) at CFG 1, fp32 (when time allows)
+  7b.1024.s30.g6.f32.final     7B at CFG 6 (configs[1] itself), fp32 (when time allows)
   10b.1024.s30.g1.bf16.final   CFG 1, bf16 (when time allows)
-  7b.1024.s30.g6.f32.final     7B at CFG 6, fp32 (when time allows)
   {key}.image                  uint8 [1, 1024, 1024, 3]: oracle/vae_ref.py (the restated Flux decoder, seed-0
                                generator weights) on that trajectory's final latents + pipeline.py:324-326; the
                                bf16 runs' images give the reference's own image-space floor (meta *.image_bf16_vs_f32).
@@ -65,8 +65,8 @@ TRAJ = [("10b.1024.s30.g1.f32", 1.0, torch.float32, True),
         ("10b.1024.s30.g6.f32", 6.0, torch.float32, False),
         ("10b.1024.s30.g6.bf16", 6.0, torch.bfloat16, False),
         ("7b.1024.s30.g1.f32", 1.0, torch.float32, True),
-        ("10b.1024.s30.g1.bf16", 1.0, torch.bfloat16, True),
-        ("7b.1024.s30.g6.f32", 6.0, torch.float32, False)]
+        ("7b.1024.s30.g6.f32", 6.0, torch.float32, False),
+        ("10b.1024.s30.g1.bf16", 1.0, torch.bfloat16, True)]
 
 
 def _digest(*ts):
