@@ -20,7 +20,8 @@ import torch  # noqa: E402
 
 from f_lite import _native as nat  # noqa: E402
 
-CLASSES = ["qkv", "rope_qknorm", "attn_self", "proj", "rmsnorm_mod", "cross_q", "attn_cross", "gateup", "down"]
+CLASSES = ["qkv", "rope_qknorm", "attn_self", "proj", "rmsnorm_mod", "cross_q", "attn_cross", "attn_cross_c", "gateup",
+           "down"]
 
 
 def main():
@@ -82,6 +83,10 @@ def main():
             kv3 = kv.view(B * LC, 2, H, HD)
             nat.attn_varlen(q3[:, 0], kv3[:, 0], kv3[:, 1], cu, cu_c, T, HD ** -0.5, out=obuf.view(M, H, HD),
                             max_score=16.5, workspace=aws, max_k=LC)
+        elif name == "attn_cross_c":  # the uniform-context collapse's launch: the cond sequence's rows only
+            kv3 = kv.view(B * LC, 2, H, HD)
+            nat.attn_varlen(q3[T:, 0], kv3[LC:, 0], kv3[LC:, 1], cu[:2], cu_c[:2], T, HD ** -0.5,
+                            out=obuf[T:].view(T, H, HD), max_score=16.5, workspace=aws, max_k=LC)
         elif name == "gateup":
             nat.gemm(nbuf, w_gate, out=hbuf, epilogue=nat.EPI_SWIGLU_BF16, w2=w_up, workspace=gws)
         elif name == "down":

@@ -34,6 +34,7 @@ WORK = {  # class -> (kind, algorithmic amount per launch: FLOP or bytes)
     "down": ("flop", 2.0 * M * F * D),
     "attn_self": ("flop", 4.0 * B * H * T * T * HD),
     "attn_cross": ("flop", 4.0 * B * H * T * LC * HD),
+    "attn_cross_c": ("flop", 4.0 * 1 * H * T * LC * HD),  # uniform-context collapse: the cond sequence only
     "rope_qknorm": ("bytes", 2.0 * (M * 2 * D * 2)),       # q and k read + written, bf16
     "rmsnorm_mod": ("bytes", M * D * 4.0 + M * D * 2.0),   # fp32 residual in, bf16 out
 }
@@ -85,8 +86,10 @@ def mean(v):
 def main():
     out_path = sys.argv[1]
     passes = dict(a.split("=", 1) for a in sys.argv[2:])
-    classes = json.loads(os.environ.get("PMC_CLASSES", "null")) or [
-        "qkv", "rope_qknorm", "attn_self", "proj", "rmsnorm_mod", "cross_q", "attn_cross", "gateup", "down"]
+    classes = json.loads(os.environ.get("PMC_CLASSES", "null"))
+    if classes is None:  # the launch order of tools/pmc_kernels.py (marker k = classes[k])
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from pmc_kernels import CLASSES as classes
     seg = {p: segment(load_rows(d), classes) for p, d in passes.items()}
     res = {}
     for c in classes:
