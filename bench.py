@@ -204,6 +204,10 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
                    f"{per_image:.0f} s (EXTRAPOLATED from the measured components)"),
         "host": host_info(),
         "components_s": {k: round(v, 3) for k, v in res.items()},
+        # BASELINE.md §4's plan run once at this workload (`--cpu-baseline-full 2`, 16 cores): the component
+        # extrapolation above lands within ~10 % of it
+        "full_step_check": {"per_image_s": 4882, "source": "profiles/r03c/bench_cpu_baseline_full.json: 2 whole "
+                            "CFG-6 steps 324.6 s + VAE 12.2 s, x15 (10B 1024^2, 16 cores)"},
     }
 
 
