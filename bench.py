@@ -190,7 +190,7 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
             res["vae_s"] = time.perf_counter() - t0
     torch.set_num_threads(prev_threads)
     per_image = steps * (res["top_s"] + cfg["depth"] * res["block_s"]) + res["vae_s"]
-    return {
+    out = {
         "value": 1.0 / per_image,
         "unit": "images/s",
         "cores": threads,
@@ -204,11 +204,13 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
                    f"{per_image:.0f} s (EXTRAPOLATED from the measured components)"),
         "host": host_info(),
         "components_s": {k: round(v, 3) for k, v in res.items()},
-        # BASELINE.md §4's plan run once at this workload (`--cpu-baseline-full 2`, 16 cores): the component
-        # extrapolation above lands within ~10 % of it
-        "full_step_check": {"per_image_s": 4882, "source": "profiles/r03c/bench_cpu_baseline_full.json: 2 whole "
-                            "CFG-6 steps 324.6 s + VAE 12.2 s, x15 (10B 1024^2, 16 cores)"},
     }
+    if (H, W, cfg["per_block_adaln"], cfg["depth"]) == (1024, 1024, True, 40) and steps == 30 and vae is not None:
+        # BASELINE.md §4's plan, run once at this workload (`--cpu-baseline-full 2`, 16 cores): the component
+        # extrapolation above lands within ~10 % of it
+        out["full_step_check"] = {"per_image_s": 4882, "source": "profiles/r03c/bench_cpu_baseline_full.json: 2 "
+                                  "whole CFG-6 steps 324.6 s + VAE 12.2 s, x15 (10B 1024^2, 16 cores)"}
+    return out
 
 
 def cpu_baseline_full(model, vae, cfg: dict, H: int, W: int, steps: int, k_steps: int = 2):
