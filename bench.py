@@ -307,6 +307,10 @@ def main():
                     help="BASELINE configs[4]: block GEMMs on MXFP8 weights + activations (block-scaled fp8 MFMA)")
     ap.add_argument("--fp8-bf16-blocks", default="",
                     help="with --fp8: comma-separated block indices that keep bf16 GEMMs (precision policy)")
+    ap.add_argument("--negative-images", type=int, default=5, metavar="K",
+                    help="after the metric's timed images, time min(K, --steps) more with a random (non-uniform) "
+                         "negative context, as generate.py:17,84 passes a user's negative prompt: the uniform-context "
+                         "collapse is then off (value_with_negative_prompt); 0 skips it")
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
     ap.add_argument("--mode", default="replica", choices=["replica", "cfg-parallel", "sp", "sp-ring"],
                     help="replica: image i on GPU i mod N (the metric line); cfg-parallel: the two CFG branches of an "
@@ -352,7 +356,8 @@ def main():
 
     from f_lite import DiT, FLitePipeline
     from f_lite import _native as nat
-    from f_lite.distributed import broadcast_context, image_indices, max_over_ranks
+    from f_lite.distributed import (broadcast_context, image_indices, max_over_ranks, process_group_info,
+                                    timed_broadcast_context)
     from f_lite.model import PRESETS
 
     cfg = dict(PRESETS[args.model])
@@ -373,7 +378,15 @@ def main():
     ctx = torch.empty(1, 512, cfg["cross_attn_input_size"], device=dev, dtype=torch.bfloat16)
     if rank == 0:
         nat.init_param_(ctx, "synthetic.t5_context", seed=1, std=1.0)
-    broadcast_context(ctx, src=0)
+    # the context broadcast is the replica mode's one collective: timed, so a multi-GPU line says what it cost
+    bcast_ms = timed_broadcast_context(ctx, src=0)
+    # a negative prompt's embedding (generate.py:17,84 -> pipeline.py:163-168): not a context of equal rows
+    neg_ctx = None
+    if args.negative_images > 0 and args.mode == "replica":
+        neg_ctx = torch.empty_like(ctx)
+        if rank == 0:
+            nat.init_param_(neg_ctx, "synthetic.t5_negative_context", seed=3, std=1.0)
+        broadcast_context(neg_ctx, src=0)
 
     lh, lw = args.height // 8, args.width // 8
 
@@ -400,10 +413,24 @@ def main():
 
     out_type = "latent" if vae is None else "uint8"
 
-    def one_image(i):
-        return pipe(prompt_embeds=ctx, latents=latents_for(i), height=args.height, width=args.width,
-                    num_inference_steps=args.sample_steps, guidance_scale=args.guidance, output_type=out_type,
-                    num_images_per_prompt=BI, use_graph=not args.no_graph).images
+    def one_image(i, negative=None):
+        return pipe(prompt_embeds=ctx, negative_prompt_embeds=negative, latents=latents_for(i), height=args.height,
+                    width=args.width, num_inference_steps=args.sample_steps, guidance_scale=args.guidance,
+                    output_type=out_type, num_images_per_prompt=BI, use_graph=not args.no_graph).images
+
+    def timed(n, negative=None):
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for k in range(n):
+            one_image(mine[k], negative)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t
 
     mine = image_indices(n_units * (args.steps + args.warmup), unit, n_units)  # image i -> unit i mod n_units
     for w in range(args.warmup):
@@ -411,18 +438,14 @@ def main():
     kinds = {"gateup": nat.PROBE_GEMM_GATEUP, "attn": nat.PROBE_ATTN_SELF, "down": nat.PROBE_GEMM_DOWN,
              "qkv": nat.PROBE_GEMM_QKV, "step": nat.PROBE_STEP, "none": -1}
     eng = model.engine()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        img = one_image(mine[k])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(args.steps)
+    # the same workload with a user's negative prompt (no uniform-context collapse): one untimed image for the new
+    # context's set-up and graph capture, then min(K, steps) timed; reported beside the metric, never as `value`
+    neg_images, elapsed_neg = 0, None
+    if neg_ctx is not None:
+        neg_images = min(args.negative_images, args.steps)
+        one_image(mine[0], neg_ctx)
+        elapsed_neg = timed(neg_images, neg_ctx)
     # Per-launch timing of the dominant kernel: HIP event pairs on the engine stream around every launch of
     # that kernel during one more image (the same launch sequence, run eagerly: event timestamps are not
     # readable from a replayed hipGraph on ROCm 7.2).
@@ -436,6 +459,10 @@ def main():
         probe_ms = eng.read_probe(8192)
         eng.set_probe(-1, 0)
     elapsed = max_over_ranks(elapsed, device=dev)
+    if elapsed_neg is not None:
+        elapsed_neg = max_over_ranks(elapsed_neg, device=dev)
+    bcast_ms_max = max_over_ranks(bcast_ms, device=dev) if dist is not None else bcast_ms
+    pg = process_group_info()
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -463,6 +490,15 @@ def main():
     f_collapse = (args.sample_steps * cross_blocks * (2 * T * D * D + 4 * T * 512 * D + 2 * T * D * D)
                   if collapse else 0.0)
     f_image = f_ref_image - f_dedup - f_collapse
+    neg = None
+    if elapsed_neg is not None:
+        v_neg = n_units * neg_images * BI / elapsed_neg
+        neg = {"value": round(v_neg, 5), "images_per_gpu": neg_images, "ms_per_image": round(elapsed_neg / neg_images
+                                                                                           * 1000.0 / BI, 2),
+               "algorithmic_flops_per_image": f_ref_image - f_dedup,
+               "mfma_util_image": round((f_ref_image - f_dedup) * v_neg / world / PEAK_BF16, 4),
+               "context": "random [1,512,4096] negative context (not uniform): the uncond copy runs its own "
+                          "cross-attention, as with any user negative prompt (generate.py:17,84)"}
     M = 2 * BI * T
     per_launch = {
         "gateup": (2.0 * M * 2 * F * D, "SwiGLU gate/up GEMM (M=%d, N=%d, K=%d)" % (M, 2 * F, D)),
@@ -546,7 +582,13 @@ def main():
                             "sp": "context broadcast + per block an all-gather of the K/V rows, per step the output rows",
                             "sp-ring": "context broadcast + per block N-1 ring shifts of K/V rows, per step the output "
                                        "rows"}[args.mode],
-                        "images_per_unit": args.steps, "units": n_units},
+                        "images_per_unit": args.steps, "units": n_units,
+                        "process_group": pg,
+                        "context_broadcast_ms": round(bcast_ms_max, 3),
+                        "context_broadcast_note": "wall time of the [1,512,4096] bf16 context broadcast incl. the "
+                                                  "first collective's communicator set-up (max over ranks)"},
+        "value_with_negative_prompt": None if neg is None else neg["value"],
+        "negative_prompt": neg,
         "mode": args.mode,
         "latency_ms_per_image": round(elapsed / args.steps * 1000.0 / BI, 2),
         "mfma_util_image": round(f_image * value / world / PEAK_BF16, 4),

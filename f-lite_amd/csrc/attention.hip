@@ -24,6 +24,7 @@
 // same sum on every launch), normalises and stores the rows, and resets the counter for the next launch.
 #include <algorithm>
 
+#include "attn_common.h"
 #include "common.h"
 #include "fp8.h"
 #include "kernels.h"
@@ -53,81 +54,6 @@ constexpr int SPLIT_FIRST_KEYS = 16 * KT;  // below this the tail chunks go firs
 // sum and every O accumulator far inside the fp32 range for any sequence length. Larger bounds take the online
 // softmax. (The DiT's QK-normed scores: 16.5, dit.cpp kQKNormScoreBound.)
 constexpr float kMaxBoundedScore = 40.f;
-
-__device__ __forceinline__ s16x4 ds_tr16(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(p));
-}
-
-typedef __attribute__((ext_vector_type(4))) int i32x4;
-
-// Buffer descriptor (raw, stride 0) from wave-uniform values (readfirstlane makes uniformity provable).
-__device__ __forceinline__ i32x4 make_rsrc(const void* base, unsigned bytes) {
-  const unsigned long long a = (unsigned long long)base;
-  i32x4 r;
-  r.x = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
-  r.y = __builtin_amdgcn_readfirstlane((int)(a >> 32));
-  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
-  r.w = 0x00020000;
-  return r;
-}
-
-// 16-B-per-lane LDS-DMA: LDS[m0 + lane*16] = buffer[voff] (0 when voff is out of range). Inline asm on
-// purpose: hipcc counts a builtin LDS-DMA in vmcnt and then waits for it (vmcnt(0)) before every later
-// ds_read, serialising the next tile's prefetch with this tile's compute; the waits are placed by hand
-// (vmcnt(0) + barrier at the end of each tile).
-__device__ __forceinline__ void blds16(const i32x4& rsrc, unsigned voff, unsigned lds_addr) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(lds_addr)
-      : "memory");
-}
-
-// O^T += V^T . P^T with the accumulator pinned to AGPRs. Left to itself hipcc keeps O (128 registers per lane)
-// in VGPRs inside the key loop and copies it to and from AGPRs every tile (~300 v_accvgpr moves per tile,
-// an issue-bound loop). An MFMA reads its srcC from AGPRs directly. The asm is opaque to the hazard
-// recognizer, so: the first MFMA after the VALU that produced its P operand carries `s_nop 1` (VALU write ->
-// MFMA read), and every reader of O after the loop waits behind o_acc_fence() (MFMA write -> read).
-// The NOP form also "redefines" pk, so every other MFMA reading pk is ordered after it.
-template <bool NOP>
-__device__ __forceinline__ void mfma_o(f32x16& acc, const bf16x8& v, bf16x8& pk) {
-  if constexpr (NOP)
-    asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %2, %1, %0" : "+a"(acc), "+v"(pk) : "v"(v));
-  else
-    asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(v), "v"(pk));
-}
-// S^T = K . Q^T with Q^T pinned to AGPRs (loop-invariant; hipcc otherwise shuttles it between the register files
-// every tile) and S in VGPRs for the softmax VALU.
-__device__ __forceinline__ void mfma_s_first(f32x16& acc, const bf16x8& k, const bf16x8& q) {
-  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(k), "a"(q));
-}
-__device__ __forceinline__ void mfma_s(f32x16& acc, const bf16x8& k, const bf16x8& q) {
-  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(k), "a"(q));
-}
-// Wait states between an asm MFMA's write and a VALU / v_accvgpr read of its result (XDL 32x32: 18). The
-// fence "redefines" the results, so no reader can be scheduled above it.
-__device__ __forceinline__ void mfma_read_fence(f32x16& a, f32x16& b) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(a), "+v"(b));
-}
-__device__ __forceinline__ void o_acc_fence(f32x16 (&o)[8]) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
-               : "+a"(o[0]), "+a"(o[1]), "+a"(o[2]), "+a"(o[3]), "+a"(o[4]), "+a"(o[5]), "+a"(o[6]), "+a"(o[7]));
-}
-
-__device__ __forceinline__ unsigned lds_addr_of(const void* p) {
-  return (unsigned)(unsigned long long)(const LDS_AS char*)p;
-}
-
-// blockIdx -> XCD-contiguous index (bijective; the dispatcher deals blocks round-robin over the 8 XCDs)
-__device__ __forceinline__ int xcd_remap(int bid, int n) {
-  const int xcd = bid & 7, q8 = n >> 3, r8 = n & 7;
-  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-}
 
 // BOUNDED: every score s*scale is known to lie in [-max_score, max_score] (QK-normed q and k: |q|,|k| <= 16
 // for head_dim 256, so |q.k|/16 <= 16 -- model.py:180,197 precede every attention call of the DiT). Softmax is
@@ -793,6 +719,13 @@ long attn_split_workspace_bytes(int B, int H) {
   return CNT_BYTES + (long)pairs * S * SLAB_BYTES;
 }
 
+long attn_workspace_bytes(int B, int H, int max_q, int max_k) {
+  // every batch a caller of this workspace launches: B, and the deduplicated half (dit.cpp: block 0's CFG pair)
+  long n = attn_split_workspace_bytes(B, H);
+  for (int b : {B, (B + 1) / 2, 1}) n = std::max(n, attn_q256_workspace_bytes(b, H, max_q, max_k));
+  return n;
+}
+
 int attn_fwd(const AttnParams& p, hipStream_t stream) {
   FLITE_REQUIRE(p.head_dim == HD, "attention: only head_dim 256 is supported");
   FLITE_REQUIRE(p.B > 0 && p.H > 0 && p.max_q > 0, "attention: empty problem");
@@ -802,6 +735,10 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
   FLITE_REQUIRE(p.q_head_stride % 8 == 0 && p.k_head_stride % 8 == 0 && p.v_head_stride % 8 == 0,
                 "attention: head strides must be multiples of 8 elements");
   if (attn_init()) return 1;
+  {
+    const int r = attn_q256_fwd(p, stream);  // long bounded launches: 256 query rows per workgroup
+    if (r >= 0) return r;
+  }
   AttnParams q = p;
   q.n_main = (p.max_q + QT - 1) / QT;
   q.n_split = 0;

@@ -105,6 +105,11 @@ int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void
 
 long flite_attn_workspace_bytes(int batch, int num_heads) { return attn_split_workspace_bytes(batch, num_heads); }
 
+long flite_attn_workspace_bytes_for(int batch, int num_heads, int max_seqlen_q, int max_seqlen_k) {
+  if (batch <= 0 || num_heads <= 0 || max_seqlen_q < 0 || max_seqlen_k < 0) return 0;
+  return attn_workspace_bytes(batch, num_heads, max_seqlen_q, max_seqlen_k);
+}
+
 int flite_attn_varlen_fwd_ws(void* stream, const void* q, const void* k, const void* v, void* o, long q_row_stride,
                              long k_row_stride, long v_row_stride, long o_row_stride, long head_stride,
                              const int* cu_seqlens_q, const int* cu_seqlens_k, int batch, int num_heads, int head_dim,

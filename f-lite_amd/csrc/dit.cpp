@@ -283,7 +283,7 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
       FLITE_HIP_CHECK(hipMemset(sk_flags_, 0, (size_t)G * 4));
     }
   }
-  attn_ws_bytes_ = attn_split_workspace_bytes(B, H);
+  attn_ws_bytes_ = attn_workspace_bytes(B, H, Tl_, T_);  // self-attention: Tl_ queries over T_ keys
   if (attn_ws_bytes_ > 0) {
     if (alloc(&attn_ws_, (size_t)attn_ws_bytes_)) return 1;
     FLITE_HIP_CHECK(hipMemset(attn_ws_, 0, (size_t)attn_ws_bytes_));
@@ -295,7 +295,9 @@ int DitEngine::prepare(int B, int Hl, int Wl, int n_ctx_max, int n_t_max) {
   if (alloc((void**)&ctx_bad_, (long)B * 4)) return 1;
   if (alloc((void**)&ctx_c8_, (long)cfg.depth * B * D * 4)) return 1;
   if (alloc((void**)&ctx_vrow8_, (long)B * D)) return 1;
-  if (alloc((void**)&ctx_vrow8_s_, (long)(D / 128) * 256 * 4)) return 1;
+  // the collapse's M = U <= B rows: scale rows padded to the GEMM's 256-row tiles, however many sequences
+  vrow8_rows_pad_ = mx_rows_pad(B);
+  if (alloc((void**)&ctx_vrow8_s_, (long)(D / 128) * vrow8_rows_pad_ * 4)) return 1;
   ctx_uni_ = 0;
   ctx_c8_stale_ = true;
   // RoPE tables for every row a rank may hold (the last rank's padding rows read zeros)
@@ -385,6 +387,12 @@ int DitEngine::set_context(hipStream_t s, const void* ctx, const int* cu_host, i
   ctx_max_len_ = 0;
   for (int i = 0; i < nseq; ++i) ctx_max_len_ = std::max(ctx_max_len_, cu_host[i + 1] - cu_host[i]);
   if (n == 0) {
+    // no keys at all: every sequence takes the zero-key cross-attention, so no row may keep an earlier call's
+    // collapse (x += gate * c of the old context) and a cached graph holding its launch shapes must go
+    if (ctx_uni_ != 0) drop_graph();
+    ctx_uni_ = 0;
+    ctx_row0_.clear();
+    ctx_c8_stale_ = true;
     ctx_stale_ = false;
     return 0;
   }
@@ -893,14 +901,15 @@ int DitEngine::collapse_fp8(hipStream_t s) {
     for (int q = 0; q < U; ++q)
       FLITE_HIP_CHECK(hipMemcpyAsync(ctx_vrow_ + (long)q * D, ctx_kv_[i] + (long)ctx_row0_[q] * 2 * D + D,
                                      (size_t)D * 2, hipMemcpyDeviceToDevice, s));
-    if (quant_rows_fp8(ctx_vrow_, D, U, D, ctx_vrow8_, D, ctx_vrow8_s_, 256, s)) return 1;
+    FLITE_REQUIRE(U <= vrow8_rows_pad_, "collapse_fp8: more collapsed sequences than scale rows");
+    if (quant_rows_fp8(ctx_vrow_, D, U, D, ctx_vrow8_, D, ctx_vrow8_s_, vrow8_rows_pad_, s)) return 1;
     float* c8 = ctx_c8_ + (long)i * B_ * D;
     FLITE_HIP_CHECK(hipMemsetAsync(c8, 0, (size_t)U * D * 4, s));
     GemmFp8Params g;
     g.A = ctx_vrow8_;
     g.lda = D;
     g.As = ctx_vrow8_s_;
-    g.a_rows_pad = 256;
+    g.a_rows_pad = vrow8_rows_pad_;
     g.W = w8_[i].cproj;
     g.ldw = D;
     g.Ws = w8_[i].cproj_s;

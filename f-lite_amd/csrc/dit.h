@@ -129,6 +129,7 @@ class DitEngine {
   // set_context or a requantisation); only where the collapsed rows end on a 4-row boundary (uni_fp8)
   float* ctx_c8_ = nullptr;
   uint8_t *ctx_vrow8_ = nullptr, *ctx_vrow8_s_ = nullptr;
+  long vrow8_rows_pad_ = 256;  // scale rows of ctx_vrow8_s_ (mx_rows_pad(B))
   bool ctx_c8_stale_ = true;
   int collapse_fp8(hipStream_t s);
   int uni_fp8() const;

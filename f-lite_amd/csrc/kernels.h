@@ -102,6 +102,12 @@ struct AttnParams {
 int attn_fwd(const AttnParams& p, hipStream_t stream);
 // bytes of a split workspace that lets a (B sequences, H heads) launch cut its tails over the chip (0: no split)
 long attn_split_workspace_bytes(int B, int H);
+// the same for launches of up to max_q queries over up to max_k keys: also holds the 256-row kernel's split plan
+// (attention_q256.hip), which attn_fwd takes for long bounded launches when the workspace is this large
+long attn_workspace_bytes(int B, int H, int max_q, int max_k);
+// attention_q256.hip: the 256-row route (returns -1 when the launch does not qualify or the workspace is short)
+int attn_q256_fwd(const AttnParams& p, hipStream_t stream);
+long attn_q256_workspace_bytes(int B, int H, int max_q, int max_k);
 
 }  // namespace flite
 

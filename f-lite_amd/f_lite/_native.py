@@ -59,6 +59,7 @@ SIGNATURES = {
     "flite_gemm_bf16_ws": (_i, [_vp, _i, _i, _i, _vp, _l, _vp, _l, _vp, _vp, _i, _vp, _l, _vp, _l, _i, _vp]),
     "flite_attn_varlen_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _f, _f]),
     "flite_attn_workspace_bytes": (_l, [_i, _i]),
+    "flite_attn_workspace_bytes_for": (_l, [_i, _i, _i, _i]),
     "flite_attn_varlen_fwd_ws": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _i, _f,
                                       _f, _vp, _l]),
     "flite_rmsnorm_modulate": (_i, [_vp, _vp, _i, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
@@ -220,10 +221,14 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, *, out=None, epilogue=EPI_
     return out
 
 
-def attn_workspace(device, batch, num_heads):
+def attn_workspace(device, batch, num_heads, max_q=0, max_k=0):
     """Zero-filled split workspace for attn_varlen(..., workspace=) (flite_attn_workspace_bytes); None when a
-    (batch, num_heads) launch gains nothing from it."""
-    n = int(load().flite_attn_workspace_bytes(batch, num_heads))
+    (batch, num_heads) launch gains nothing from it. With max_q / max_k (flite_attn_workspace_bytes_for) it also
+    holds the 256-row kernel's split plan, which launches given max_k >= 1024 then take."""
+    if max_q or max_k:
+        n = int(load().flite_attn_workspace_bytes_for(batch, num_heads, max_q, max_k))
+    else:
+        n = int(load().flite_attn_workspace_bytes(batch, num_heads))
     return torch.zeros(n, dtype=torch.uint8, device=device) if n > 0 else None
 
 

@@ -49,6 +49,37 @@ def broadcast_context(ctx: torch.Tensor, src: int = 0, group=None) -> torch.Tens
     return ctx
 
 
+def timed_broadcast_context(ctx: torch.Tensor, src: int = 0, group=None) -> float:
+    """broadcast_context with its wall time in ms (device synchronised on both sides when ctx is on a GPU; the first
+    collective of a process group includes the communicator's set-up). bench.py records it per rank."""
+    import time
+
+    sync = torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None)
+    sync()
+    t0 = time.perf_counter()
+    broadcast_context(ctx, src=src, group=group)
+    sync()
+    return (time.perf_counter() - t0) * 1000.0
+
+
+def process_group_info(group=None):
+    """What the process group itself reports (None without one): backend, world size and rank as seen by
+    torch.distributed, and the RCCL version under the nccl backend; bench.py puts it in the line's "distributed" so a
+    multi-GPU run says what it actually ran over."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    info = {"backend": dist.get_backend(group), "world_size_seen": dist.get_world_size(group),
+            "rank_seen": dist.get_rank(group)}
+    if info["backend"] == "nccl":
+        try:
+            info["rccl_version"] = ".".join(map(str, torch.cuda.nccl.version()))
+        except Exception:  # pragma: no cover - version query unsupported
+            pass
+    return info
+
+
 def broadcast_from_group_root(t: torch.Tensor, group=None) -> torch.Tensor:
     """In-place broadcast of `t` from rank 0 OF `group` (its global rank resolved) to the group's ranks. With
     gloo (CPU tests, or two ranks sharing one GPU) a device tensor is staged through the host."""

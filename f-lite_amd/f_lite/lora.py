@@ -61,7 +61,11 @@ def merge_lora_(model: torch.nn.Module, state_dict: Dict[str, torch.Tensor], sca
     first restored to its base weight (kept on the host at the first merge), so loading the same file twice leaves
     the weights bit-identical, and a second adapter does not stack on the first. Modules the new file does not name
     keep the adapter they had, as peft's do. If a merged weight was overwritten since (load_state_dict, random_init_),
-    its current value is taken as the new base.
+    its current value is taken as the new base. "Still holds our merge" is decided by the weight's CONTENT (a 64-bit
+    fingerprint of its bits recorded after the merge), not by its version counter or storage pointer: a write through
+    `p.data` (which bumps no version) is seen, and a `.to(device)` after the merge (new pointer, same bits) still
+    restores the kept base. Cost: the base of every merged module stays on the host (bf16: 2 bytes per weight) for
+    the model's lifetime, which is what makes a reload bit-identical rather than W - B@A rounded twice.
 
     Adapters on modules that do not exist or that `target_modules` does not select are skipped with a warning (peft
     loads with strict=False and reports them as unexpected keys). A shape or rank mismatch raises: peft would
@@ -93,15 +97,27 @@ def merge_lora_(model: torch.nn.Module, state_dict: Dict[str, torch.Tensor], sca
     for mod, lin, A, B in todo:
         W = lin.weight
         rec = merged.get(mod)
-        if rec is not None and rec["version"] == W._version and rec["ptr"] == W.data_ptr():
+        if rec is not None and rec["fp"] == _fingerprint(W):
             base = rec["base"]  # the weight still holds our merge: start from the kept base
         else:
             base = W.detach().to("cpu", copy=True)
         delta = B.to(W.device, torch.float32) @ A.to(W.device, torch.float32)
         W.copy_((base.to(W.device, torch.float32) + scaling * delta).to(W.dtype))
         merged[mod] = {"A": A.detach().cpu(), "B": B.detach().cpu(), "scaling": scaling, "base": base,
-                       "version": W._version, "ptr": W.data_ptr()}
+                       "fp": _fingerprint(W)}
     return len(todo)
+
+
+_INT_OF = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
+
+
+def _fingerprint(W: torch.Tensor) -> Tuple[int, int, int]:
+    """Position-weighted 64-bit sums of the tensor's raw bits (wrapping), on its own device: equal contents give equal
+    fingerprints wherever the tensor lives; a changed element changes them but for a 2^-64-scale accident."""
+    bits = W.detach().contiguous().reshape(-1).view(_INT_OF[W.element_size()]).to(torch.int64)
+    idx = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64)
+    mult = (idx * 2654435761 + 97) % 2147483629 + 1
+    return (int(bits.sum()), int((bits * mult).sum()), int((bits * bits * (idx % 8191 + 1)).sum()))
 
 
 def merged_state_dict(model: torch.nn.Module) -> Dict[str, torch.Tensor]:

@@ -11,6 +11,9 @@
                the CU's texture path (64 KiB of pieces per 64-key tile at 64 B/clk = 1024 of the tile's 2048 MFMA
                cycles). V_{j+1} lands in the V buffer phase B of iteration j does NOT read (last read in j - 1,
                before its barrier), and the end-of-iteration vmcnt(0) + barrier publishes it as before.
+
+The round-4 --qscale (pre-scaled Q^T, no shift) and --ldelay (row sum one score late) variants are in the product
+source since round 4 (profiles/r04b), so they are no longer patches; profiles/r04b's baseline is that commit's parent.
 """
 import subprocess
 import sys
@@ -19,7 +22,7 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 
 
-def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False, qlate=False, packdelay=False, split=None):
+def make(name, kspread=False, vdma_b=None, qlate=False, packdelay=False, split=None):
     src = (HERE.parent / "csrc" / "attention.hip").read_text()
 
     def sub(old, new, count=1):
@@ -49,29 +52,6 @@ def make(name, kspread=False, vdma_b=None, qscale=False, ldelay=False, qlate=Fal
             blds16(krs, k_src[''' + k_idx + '''], lds0 + DKB * TILE + (wave * 8 + ''' + k_idx + ''') * 1024 + K_OFF);''' +
         v_part + '''
         }''')
-    if qscale:  # bounded path: Q^T pre-scaled by scale*log2(e) at load (one bf16 rounding, as q's own), no shift:
-        # p = exp2(s'), one v_exp per score instead of v_fma + v_exp (|s'| <= 23.8: p in [2^-23.8, 2^23.8])
-        sub("    for (int s = 0; s < 16; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);\n",
-            "    for (int s = 0; s < 16; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);\n"
-            "    if constexpr (BOUNDED) {\n"
-            "      const float qs = p.scale * 1.4426950408889634f;\n"
-            "#pragma unroll\n"
-            "      for (int s = 0; s < 16; ++s)\n"
-            "#pragma unroll\n"
-            "        for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * qs);\n"
-            "    }\n")
-        sub("  float m_run = BOUNDED ? p.max_score * 1.4426950408889634f : -1e30f;",
-            "  float m_run = BOUNDED ? 0.f : -1e30f;")
-        sub("      const float v = __builtin_amdgcn_exp2f(sacc[r] * sl2 - m_run);",
-            "      const float v = __builtin_amdgcn_exp2f(sacc[r]);")
-    if ldelay:  # row sum: add the PREVIOUS element's p (same adds, same order: bit-identical), so the v_add no
-        # longer waits on the v_exp just issued (the trans -> VALU forwarding hazard cost an s_nop per element)
-        sub("      l_run += v;\n      if (e & 1) {", "      l_run += e_prev;\n      if (e & 1) {")
-        sub("        if constexpr (EX) softmax_elem(pn, m, e_prev);\n        __builtin_amdgcn_sched_barrier(0);\n      }\n",
-            "        if constexpr (EX) softmax_elem(pn, m, e_prev);\n        __builtin_amdgcn_sched_barrier(0);\n      }\n"
-            "      if constexpr (EX) l_run += e_prev;\n")
-        sub("        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);\n",
-            "        for (int e = 0; e < 32; ++e) softmax_elem(pa, e, e_prev);\n        l_run += e_prev;\n")
     if qlate:  # Q^T moves to AGPRs (which waits for its loads) only AFTER the K_0 / V_0 / K_1 copies are issued,
         # so the prologue pays max(Q latency, K/V latency) instead of their sum
         pin = ("    if constexpr (BOUNDED) {  // move Q^T into AGPRs here, then clear the write -> MFMA-read hazard\n"
@@ -237,6 +217,5 @@ if __name__ == "__main__":
     vb = None
     if "--vdma-b" in a:
         vb = int(a[a.index("--vdma-b") + 1])
-    make(name, kspread="--kspread" in a, vdma_b=vb, qscale="--qscale" in a, ldelay="--ldelay" in a,
-         qlate="--qlate" in a, packdelay="--packdelay" in a,
+    make(name, kspread="--kspread" in a, vdma_b=vb, qlate="--qlate" in a, packdelay="--packdelay" in a,
          split=a[a.index("--split") + 1] if "--split" in a else None)

@@ -83,6 +83,14 @@ int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void
 long flite_attn_workspace_bytes(int batch, int num_heads);
 
 /*
+ * The same for launches of up to max_seqlen_q queries over up to max_seqlen_k keys per sequence: also large enough
+ * for the 256-query-row kernel's split plan, which flite_attn_varlen_fwd_ws takes for bounded launches over long
+ * key ranges (max_seqlen_k >= 1024 given; the DiT's self-attention, reference f_lite/model.py:203-210). Always
+ * >= flite_attn_workspace_bytes(batch, num_heads).
+ */
+long flite_attn_workspace_bytes_for(int batch, int num_heads, int max_seqlen_q, int max_seqlen_k);
+
+/*
  * flite_attn_varlen_fwd with a caller-owned split workspace (device memory, zero-filled once, left zeroed by
  * every launch; launches sharing it must be stream-ordered). With max_score > 0 the partial last q-tile of each
  * (sequence, head) is cut over the chip by key ranges and reduced in a fixed order (deterministic).

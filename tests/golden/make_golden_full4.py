@@ -19,6 +19,7 @@ Fixtures (tests/golden/golden_full4.safetensors) + golden_full4_meta.json:
   7b.1024.s30.g1.f32.final     BASELINE configs[1]'s model (7B, model.py layout) at CFG 1, fp32 (when time allows)
   7b.1024.s30.g6.f32.final     7B at CFG 6 (configs[1] itself), fp32 (when time allows)
   10b.1024.s30.g1.bf16.final   CFG 1, bf16 (when time allows)
+  7b.1024.s30.g6.bf16.final    configs[1] in the reference's bf16 arithmetic: the configs[1] floor (round 5)
   {key}.image                  uint8 [1, 1024, 1024, 3]: oracle/vae_ref.py (the restated Flux decoder, seed-0
                                generator weights) on that trajectory's final latents + pipeline.py:324-326; the
                                bf16 runs' images give the reference's own image-space floor (meta *.image_bf16_vs_f32).
@@ -66,7 +67,8 @@ TRAJ = [("10b.1024.s30.g1.f32", 1.0, torch.float32, True),
         ("10b.1024.s30.g6.bf16", 6.0, torch.bfloat16, False),
         ("7b.1024.s30.g1.f32", 1.0, torch.float32, True),
         ("7b.1024.s30.g6.f32", 6.0, torch.float32, False),
-        ("10b.1024.s30.g1.bf16", 1.0, torch.bfloat16, True)]
+        ("10b.1024.s30.g1.bf16", 1.0, torch.bfloat16, True),
+        ("7b.1024.s30.g6.bf16", 6.0, torch.bfloat16, False)]
 
 
 def _digest(*ts):

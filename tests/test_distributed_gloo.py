@@ -20,15 +20,16 @@ def _free_port():
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from f_lite.distributed import broadcast_context, image_indices, max_over_ranks
+    from f_lite.distributed import image_indices, max_over_ranks, process_group_info, timed_broadcast_context
 
     ctx = torch.full((1, 8, 16), float(rank + 1))
     if rank == 0:
         ctx = torch.arange(128, dtype=torch.float32).reshape(1, 8, 16)
-    broadcast_context(ctx, src=0)
+    # bench.py's path: the timed context broadcast, then what the process group reports about itself
+    ms = timed_broadcast_context(ctx, src=0)
     mine = image_indices(8, rank, world)
     t = max_over_ranks(1.0 + rank)
-    q.put((rank, ctx.sum().item(), mine, t))
+    q.put((rank, ctx.sum().item(), mine, t, ms, process_group_info()))
     dist.destroy_process_group()
 
 
@@ -160,9 +161,11 @@ def test_sharding_and_broadcast(world):
         p.join(60)
     expect = float(sum(range(128)))
     shards = []
-    for rank, s, mine, t in res:
+    for rank, s, mine, t, ms, pg in res:
         assert s == expect  # every rank sees rank 0's context
         assert t == float(world)  # slowest rank's time
+        assert ms >= 0.0
+        assert pg == {"backend": "gloo", "world_size_seen": world, "rank_seen": rank}
         shards += mine
     assert sorted(shards) == list(range(8))  # every image exactly once
 

@@ -363,3 +363,21 @@ def test_uniform_context_collapse_matches_full_computation(tmp_path):
         pc, pf = psnr(col[f"{name}.zero.True"], ref), psnr(full[f"{name}.zero.True"], ref)
         print(f"{name}, zero negative, vs the fp32 oracle: collapse {pc:.2f} dB, full computation {pf:.2f} dB")
         assert pc >= 35.0 and pc >= pf - 0.3
+
+
+def test_empty_context_after_collapsed_context(golden):
+    """dit.cpp set_context with no context keys at all (an all-zero mask) after a call whose zero context was collapsed
+    (ADVICE r04 medium): the empty call must clear the collapse, so the forward equals a fresh engine's forward with
+    the same empty context bit for bit, and differs from the collapsed one."""
+    x, ctx = _inputs(golden)
+    t = golden["in.t"].to(DEV)
+    x = x.to(DEV)
+    zero = torch.zeros_like(ctx).to(DEV)
+    none = torch.zeros(ctx.shape[0], ctx.shape[1], dtype=torch.int32, device=DEV)
+    m = DiT.random(seed=0, **PRESETS["tiny"])
+    collapsed = m(x, zero, None, t, output_dtype=torch.float32)
+    after = m(x, zero, none, t, output_dtype=torch.float32)
+    fresh = DiT.random(seed=0, **PRESETS["tiny"])(x, zero, none, t, output_dtype=torch.float32)
+    assert torch.isfinite(after).all()
+    assert torch.equal(after, fresh)
+    assert not torch.equal(after, collapsed)

@@ -288,8 +288,7 @@ def test_10b_1024_30_steps_vs_reference(gold4, m7b, m10b, name, g):
 
     gd, meta = gold4
     key = f"{name}.1024.s30.g{g:g}"
-    if f"{key}.f32.final" not in gd:
-        pytest.skip(f"{key} not in the fixture file yet")
+    assert f"{key}.f32.final" in gd, f"{key}.f32.final missing from golden_full4.safetensors"
     pipe = FLitePipeline(m7b if name == "7b" else m10b, vae=AutoencoderKL.random(seed=0))
     assert (pipe.vae.config.scaling_factor, pipe.vae.config.shift_factor) == (SCALING, SHIFT)
     kw = dict(prompt_embeds=hashed(meta, "ctx"), latents=hashed(meta, "latents_1024"), height=1024, width=1024,
@@ -299,19 +298,25 @@ def test_10b_1024_30_steps_vs_reference(gold4, m7b, m10b, name, g):
     floor = meta.get(f"{key}.bf16_vs_f32_psnr")
     print(f"{name} 1024^2 30-step CFG-{g:g} final latents: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
           f"{'n/a' if floor is None else f'{floor:.2f} dB'})")
-    if floor is not None:
-        assert p >= floor
     if g == 1.0:
-        assert p >= 40.0
-    if f"{key}.f32.image" in gd:
-        img = pipe(**kw, output_type="uint8").images.cpu()
-        ref = gd[f"{key}.f32.image"]
-        assert img.shape == ref.shape == (1, 1024, 1024, 3)
-        pi = 10 * math.log10(255.0 ** 2 / max((img.double() - ref.double()).pow(2).mean().item(), 1e-12))
-        ifloor = meta.get(f"{key}.image_bf16_vs_f32_psnr")
-        print(f"  uint8 image (HIP loop + HIP VAE) vs oracle VAE on the reference latents: {pi:.2f} dB (the "
-              f"reference's own bf16 run: {'n/a' if ifloor is None else f'{ifloor:.2f} dB'})")
-        if g == 1.0:
-            assert pi >= 40.0  # the bar applies as stated where CFG 6 does not amplify the noise
-        elif ifloor is not None:
-            assert pi >= ifloor
+        assert p >= 40.0  # SURVEY §8d as stated; the reference's own bf16 run, where generated, as well
+        if floor is not None:
+            assert p >= floor
+    else:
+        # CFG 6 amplifies every rounding along the trajectory, so the bar is the reference's own bf16 run of the same
+        # 30 steps; a CFG-6 case without that floor is a missing fixture, never "no assertion" 
+        assert floor is not None, f"{key}.bf16_vs_f32_psnr missing: run make_golden_full4.py --only {key}.bf16"
+        assert p >= floor
+    assert f"{key}.f32.image" in gd, f"{key}.f32.image missing: run make_golden_full4.py (it decodes every final)"
+    img = pipe(**kw, output_type="uint8").images.cpu()
+    ref = gd[f"{key}.f32.image"]
+    assert img.shape == ref.shape == (1, 1024, 1024, 3)
+    pi = 10 * math.log10(255.0 ** 2 / max((img.double() - ref.double()).pow(2).mean().item(), 1e-12))
+    ifloor = meta.get(f"{key}.image_bf16_vs_f32_psnr")
+    print(f"  uint8 image (HIP loop + HIP VAE) vs oracle VAE on the reference latents: {pi:.2f} dB (the "
+          f"reference's own bf16 run: {'n/a' if ifloor is None else f'{ifloor:.2f} dB'})")
+    if g == 1.0:
+        assert pi >= 40.0  # the bar applies as stated where CFG 6 does not amplify the noise
+    else:
+        assert ifloor is not None, f"{key}.image_bf16_vs_f32_psnr missing: the bf16 trajectory's image"
+        assert pi >= ifloor

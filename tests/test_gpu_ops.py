@@ -349,3 +349,39 @@ def test_init_param_bit_exact():
         tb = torch.empty(n, device=DEV, dtype=torch.bfloat16)
         nat.init_param_(tb, name, seed=3, std=std)
         assert torch.equal(tb.cpu(), ref.bfloat16())
+
+
+# The 256-query-row kernel (attention_q256.hip): bounded launches over >= 1024 keys with a workspace sized by
+# attn_workspace(..., max_q, max_k) and max_k given. Its plan runs some full q-tiles whole, others as two key halves,
+# and the tail rows as key chunks. Against the fp32 reference and the 128-row kernel (same launch without max_k).
+# Cases: the DiT self-attention (T = 4112, 16-row tails), the 1344x896 length (T = 4720, 112-row tails), one sequence
+# (every full tile split), unequal lengths (a short sequence's q-tiles and tails end early), a length that is a
+# multiple of 256 (no tail), a key range not a multiple of 32, cross-shaped keys.
+@pytest.mark.parametrize("lens_q,lens_k,H", [([4112, 4112], None, 12), ([4720], None, 4), ([1300], None, 1),
+                                             ([3000, 1500], None, 3), ([2048], None, 2), ([700, 900], [1100, 1037], 2),
+                                             ([4112], [1536], 12)])
+def test_attention_q256(lens_q, lens_k, H):
+    D = 256
+    lens_k = lens_q if lens_k is None else lens_k
+    B = len(lens_q)
+    ws = nat.attn_workspace(DEV, B, H, max(lens_q), max(lens_k))
+    old_ws = nat.attn_workspace(DEV, B, H)
+    assert ws is not None and (old_ws is None or ws.numel() >= old_ws.numel())
+    cu_q = torch.tensor([0] + list(torch.tensor(lens_q).cumsum(0)), dtype=torch.int32)
+    cu_k = torch.tensor([0] + list(torch.tensor(lens_k).cumsum(0)), dtype=torch.int32)
+    g = torch.Generator(device=DEV).manual_seed(sum(lens_q) + 7 * H)
+    q = R.own_rmsnorm(torch.randn(int(cu_q[-1]), H, D, device=DEV, generator=g), None).bfloat16()
+    k = R.own_rmsnorm(torch.randn(int(cu_k[-1]), H, D, device=DEV, generator=g), None).bfloat16()
+    v = torch.randn(int(cu_k[-1]), H, D, device=DEV, generator=g).bfloat16()
+    args = (q, k, v, cu_q.to(DEV), cu_k.to(DEV), max(lens_q), D ** -0.5)
+    new = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
+    old = nat.attn_varlen(*args, max_score=16.5, workspace=ws)  # no max_k: the 128-row kernel
+    assert torch.isfinite(new.float()).all()
+    if sum(lens_q) * H * max(lens_k) <= 2 * 4112 * 4112 * 2:
+        ref = _attn_ref(q, k, v, cu_q, cu_k, D ** -0.5)
+        assert rel(new, ref) < 1e-2
+        print(f"q256 {lens_q} x {lens_k} H={H}: rel vs fp32 {rel(new, ref):.2e} (128-row kernel {rel(old, ref):.2e})")
+    assert rel(new, old) < 5e-3  # same math; split halves and chunk sums change the summation order only
+    again = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
+    assert torch.equal(new, again)  # deterministic whichever split piece arrives last
+    assert int(ws[:16384].view(torch.int32).abs().sum().item()) == 0  # counters left zeroed

@@ -213,6 +213,17 @@ def test_lora_load_replaces_like_peft(tmp_path):
     k = next(k for k in a2 if k.endswith("lora_A.weight")).replace(".lora_A.weight", "")
     want = (base[k + ".weight"].float() + a2[k + ".lora_B.weight"] @ a2[k + ".lora_A.weight"]).bfloat16()
     assert torch.equal(m.state_dict()[k + ".weight"], want)
+    # "still holds our merge" is decided by content. A move to new storage after the merge (same bits,
+    # new pointer; .to(device) on a GPU) still restores the kept base, so reloading stays bit-identical ...
+    m.to(torch.float32).to(torch.bfloat16)
+    merge_lora_(m, a2)
+    assert torch.equal(m.state_dict()[k + ".weight"], want)
+    # ... and a write through .data (no version bump) becomes the new base instead of being silently undone
+    W = dict(m.named_modules())[k].weight
+    W.data.copy_(base[k + ".weight"] * 2)
+    merge_lora_(m, a2)
+    want2 = ((base[k + ".weight"] * 2).float() + a2[k + ".lora_B.weight"] @ a2[k + ".lora_A.weight"]).bfloat16()
+    assert torch.equal(m.state_dict()[k + ".weight"], want2)
 
 
 def test_weights_updated_bumps_generation():
