@@ -311,6 +311,9 @@ def main():
                     help="after the metric's timed images, time min(K, --steps) more with a random (non-uniform) "
                          "negative context, as generate.py:17,84 passes a user's negative prompt: the uniform-context "
                          "collapse is then off (value_with_negative_prompt); 0 skips it")
+    ap.add_argument("--fp8-classes", default="all",
+                    help="with --fp8: GEMM classes on MXFP8 (comma-separated _native.FP8_CLASSES names: qkv, proj, "
+                         "cross_q, cross_proj, gate_up, down; 'all'), the others bf16 (precision policy)")
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
     ap.add_argument("--mode", default="replica", choices=["replica", "cfg-parallel", "sp", "sp-ring"],
                     help="replica: image i on GPU i mod N (the metric line); cfg-parallel: the two CFG branches of an "
@@ -364,7 +367,7 @@ def main():
     model = DiT.random(seed=0, device=dev, **cfg)
     keep16 = [int(b) for b in args.fp8_bf16_blocks.split(",") if b.strip()]
     if args.fp8:
-        model.enable_fp8(True, bf16_blocks=keep16)
+        model.enable_fp8(True, bf16_blocks=keep16, gemm_classes=args.fp8_classes)
     vae = None
     if not args.no_vae:
         from f_lite.vae import AutoencoderKL
@@ -512,7 +515,8 @@ def main():
         avg_ms = sum(probe_ms) / len(probe_ms)
         flops, what = per_launch[args.probe]
         achieved = flops / (avg_ms * 1e-3) / 1e12
-        fp8_kernel = args.fp8 and args.probe in ("gateup", "down", "qkv")
+        cls = {"gateup": "gate_up", "down": "down", "qkv": "qkv"}.get(args.probe)
+        fp8_kernel = args.fp8 and cls is not None and bool(nat.fp8_class_mask(args.fp8_classes) & nat.FP8_CLASSES[cls])
         peak = PEAK_FP8 if fp8_kernel else PEAK_BF16
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak / 1e12, 1),
                     "unit": "TFLOP/s", "frac": round(achieved * 1e12 / peak, 4), "traffic": None,
@@ -571,7 +575,8 @@ def main():
                                    "sp": "sequence parallel sp%d (K/V all-gather per block)" % world,
                                    "sp-ring": "sequence parallel sp%d (ring K/V shifts)" % world}[args.mode],
                    "hipgraph": not args.no_graph, "vae_tiling": bool(args.vae_tiling),
-                   "fp8_bf16_blocks": keep16 if args.fp8 else None},
+                   "fp8_bf16_blocks": keep16 if args.fp8 else None,
+                   "fp8_classes": args.fp8_classes if args.fp8 else None},
         "distributed": {"world_size": world,
                         "backend": ("gloo REHEARSAL (ranks share %d GPU(s); not a measurement)"
                                     % torch.cuda.device_count() if rehearsal else

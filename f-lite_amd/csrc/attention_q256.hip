@@ -22,6 +22,7 @@
 // order (deterministic) and normalises. The bounded softmax has no running max, so partial sums add without any
 // rescale. The split counts come from a list-scheduling simulation of the hardware dispatcher (q256_plan).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -287,11 +288,11 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
       __builtin_amdgcn_sched_barrier(0);
       const s16x8 c = __builtin_shufflevector(lo[f], hi[f], 0, 1, 2, 3, 4, 5, 6, 7);
       const bf16x8 vf = __builtin_bit_cast(bf16x8, c);
+      // P was packed a whole phase A earlier (no VALU -> MFMA hazard left to clear), and it is read in place: the
+      // NOP form's "+v" operand made hipcc copy each block's P into one register set right behind the previous
+      // MFMA reading it (v_mov_b64 + s_nop 1), which returned the other block's P for the second MFMA
       bf16x8 pk = __builtin_bit_cast(bf16x8, pc[qb * 2 + s]);
-      if (dt == 0)
-        mfma_o<true>(o_acc[qb * 8 + dt], vf, pk);
-      else
-        mfma_o<false>(o_acc[qb * 8 + dt], vf, pk);
+      mfma_o<false>(o_acc[qb * 8 + dt], vf, pk);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (EX) softmax_elem(pn, m, e_prev);
       __builtin_amdgcn_sched_barrier(0);
@@ -548,6 +549,15 @@ Plan make_plan(int cus, int pairs, int max_q, int max_k) {
       }
     }
   }
+  // diagnostic A/B switch: FLITE_Q256_PLAN="<split tiles>,<tail chunks>" (clamped to the launch's tiles)
+  if (const char* f = getenv("FLITE_Q256_PLAN")) {
+    int hs = 0, ts = 1;
+    if (sscanf(f, "%d,%d", &hs, &ts) == 2) {
+      pl.n_half = std::max(0, std::min(hs, F));
+      pl.n_whole = F - pl.n_half;
+      pl.n_tail = tail_rows > 0 ? std::max(1, std::min(ts, MAX_TAIL)) : 0;
+    }
+  }
   pl.ws_bytes = CNT_BYTES + ((long)pl.n_half * 2 + (long)pairs * pl.n_tail) * SLAB_BYTES;
   return pl;
 }
@@ -557,6 +567,7 @@ std::map<std::tuple<int, int, int, int>, Plan> g_plans;
 bool g_q256_attr = false;
 int g_q256_cus = 0;
 int g_q256_off = -1;
+int g_min_keys = MIN_KEYS;
 
 int q256_init() {
   if (g_q256_attr) return 0;
@@ -567,6 +578,7 @@ int q256_init() {
   FLITE_HIP_CHECK(hipDeviceGetAttribute(&g_q256_cus, hipDeviceAttributeMultiprocessorCount, dev));
   const char* off = getenv("FLITE_NO_ATTN_Q256");  // A/B switch: every attention on the 128-row kernel
   g_q256_off = off && off[0] == '1';
+  if (const char* mk = getenv("FLITE_Q256_MIN_KEYS")) g_min_keys = std::max(KT, atoi(mk));  // A/B: key-range floor
   g_q256_attr = true;
   return 0;
 }
@@ -585,11 +597,11 @@ const Plan* plan_for(int pairs, int max_q, int max_k) {
 bool attn_q256_eligible(const AttnParams& p) {
   if (q256_init() || g_q256_off) return false;
   return p.head_dim == HD && p.max_score > 0.f && p.part_mode == 0 && !p.o8 && !p.k_end && p.split_ws &&
-         p.max_q >= QT && p.max_k >= MIN_KEYS && p.B * p.H * (p.max_q / QT) <= (int)(CNT_BYTES / 4) - p.B * p.H;
+         p.max_q >= QT && p.max_k >= g_min_keys && p.B * p.H * (p.max_q / QT) <= (int)(CNT_BYTES / 4) - p.B * p.H;
 }
 
 long attn_q256_workspace_bytes(int B, int H, int max_q, int max_k) {
-  if (max_q < QT || max_k < MIN_KEYS) return 0;
+  if (q256_init() || max_q < QT || max_k < g_min_keys) return 0;
   const Plan* pl = plan_for(B * H, max_q, max_k);
   return pl ? pl->ws_bytes : 0;
 }

@@ -489,6 +489,11 @@ int flite_dit_set_fp8_bf16_blocks(flite_dit* dit, const int* blocks, int n) {
   return dit->eng->set_fp8_bf16_blocks(blocks, n);
 }
 
+int flite_dit_set_fp8_gemm_classes(flite_dit* dit, int mask) {
+  FLITE_REQUIRE(dit, "flite_dit_set_fp8_gemm_classes: null engine");
+  return dit->eng->set_fp8_classes(mask);
+}
+
 int flite_dit_weights_updated(flite_dit* dit, void* stream) {
   FLITE_REQUIRE(dit, "flite_dit_weights_updated: null engine");
   return dit->eng->weights_updated((hipStream_t)stream);

@@ -842,6 +842,13 @@ int DitEngine::set_fp8_bf16_blocks(const int* blocks, int n) {
   return 0;
 }
 
+int DitEngine::set_fp8_classes(int mask) {
+  FLITE_REQUIRE(mask >= 0 && mask <= FLITE_FP8_ALL, "set_fp8_gemm_classes: mask outside FLITE_FP8_ALL");
+  if (mask != fp8_classes_) drop_graph();  // a cached graph holds the old choice
+  fp8_classes_ = mask;
+  return 0;
+}
+
 int DitEngine::weights_updated(hipStream_t s) {
   w8_stale_ = true;
   ctx_stale_ = true;
@@ -991,7 +998,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     g.sk_flags = no_sk ? nullptr : sk_flags_;
     return gemm_fp8(g, epi, s);
   };
-  auto attn = [&](const bf16_t* qp, long ldq, const bf16_t* kp, const bf16_t* vp, long ldkv, const int* cu_k,
+  auto attn = [&](bool mx, const bf16_t* qp, long ldq, const bf16_t* kp, const bf16_t* vp, long ldkv, const int* cu_k,
                   int max_k, int nseq = 0, int seq0 = 0) -> int {
     AttnParams a;
     a.q = qp;
@@ -1013,7 +1020,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     a.max_score = kQKNormScoreBound;
     a.split_ws = attn_ws_;
     a.split_ws_bytes = attn_ws_bytes_;
-    if (attn_mx_) {  // the proj GEMM's MXFP8 A operand straight from the attention epilogue
+    if (mx) {  // the proj GEMM's MXFP8 A operand straight from the attention epilogue
       a.o8 = obuf8_;
       a.o8_scale = obuf8_s_;
       a.o8_rows_pad = mpad_;
@@ -1034,47 +1041,153 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     }
     return rope_qknorm(rn, s);
   };
-  // --- self attention ---
-  if (norm8(b.norm1, shift_sa, scale_sa, Msa)) return 1;
-  if (probe_sa && probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
+  // the GEMM classes on MXFP8 (flite_dit_set_fp8_gemm_classes); every other class runs its bf16 GEMM, and each
+  // activation is produced in the format its consumer takes
+  const int cm = fp8_classes_;
+  const bool f_qkv = cm & FLITE_FP8_QKV, f_proj = cm & FLITE_FP8_PROJ, f_cq = cm & FLITE_FP8_CROSS_Q,
+             f_cproj = cm & FLITE_FP8_CROSS_PROJ, f_gu = cm & FLITE_FP8_GATE_UP, f_down = cm & FLITE_FP8_DOWN;
+  auto norm16 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0, long r0 = 0) -> int {
+    NormModParams nm;
+    nm.x = x_ + r0 * D;
+    nm.ldx = D;
+    nm.y = nbuf_ + r0 * D;
+    nm.ldy = D;
+    nm.w = w;
+    nm.shift = sh;
+    nm.scale = sc;
+    nm.mod_seg_stride = mseg;
+    nm.rows = rows > 0 ? rows : M_ - r0;
+    nm.D = D;
+    nm.in_seg = Tl_;
+    nm.in_stride = Tl_;
+    nm.in_off = 0;
+    return rmsnorm_mod(nm, false, s);
+  };
+  auto g16 = [&](const bf16_t* A, const bf16_t* W, int N, const bf16_t* bias, int epi, void* out, long ldo,
+                 const float* gate, int norm_cols = 0, int rope_cols = 0, long rows = 0) -> int {
+    GemmParams g;
+    g.A = A;
+    g.lda = D;
+    g.W = W;
+    g.ldw = D;
+    g.bias = bias;
+    g.out = out;
+    g.ldo = ldo;
+    g.gate = gate;
+    g.gate_seg_stride = mseg;
+    g.rows_per_seg = Tl_;
+    g.M = (int)(rows > 0 ? rows : M_);
+    g.N = N;
+    g.K = D;
+    g.rope = rope_axes();
+    g.norm_cols = norm_cols;
+    g.rope_cols = rope_cols;
+    return gemm(g, epi, s);
+  };
   const bool fused = fuse_qk_norm();  // RoPE + QK-norm in the GEMM epilogue (the weights were quantised to match)
-  if (g8(nbuf8_, nbuf8_s_, q.qkv, q.qkv_s, 3L * D, 3 * D, D, b.qkv_b, fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16,
-         qkv_, 3L * D, nullptr, 2 * D, cfg.use_rope ? 2 * D : 0, Msa))
+  // --- self attention ---
+  if (f_qkv ? norm8(b.norm1, shift_sa, scale_sa, Msa) : norm16(b.norm1, shift_sa, scale_sa, Msa)) return 1;
+  if (probe_sa && probe_begin(s, FLITE_PROBE_GEMM_QKV)) return 1;
+  if (f_qkv) {
+    if (g8(nbuf8_, nbuf8_s_, q.qkv, q.qkv_s, 3L * D, 3 * D, D, b.qkv_b, fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16,
+           qkv_, 3L * D, nullptr, 2 * D, cfg.use_rope ? 2 * D : 0, Msa))
+      return 1;
+  } else if (g16(nbuf_, b.qkv_w, 3 * D, b.qkv_b, fused ? EPI_QKV_NORM_BF16 : EPI_STORE_BF16, qkv_, 3L * D, nullptr,
+                 2 * D, cfg.use_rope ? 2 * D : 0, Msa)) {
     return 1;
+  }
   if (probe_sa && probe_end(s, FLITE_PROBE_GEMM_QKV)) return 1;
   if (!fused && qk_norm(3L * D, 2 * H, cfg.use_rope ? 2 * H : 0, Msa)) return 1;
   if (probe_sa && probe_begin(s, FLITE_PROBE_ATTN_SELF)) return 1;
-  if (attn(qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, Tl_, Bsa)) return 1;
+  if (attn(f_proj && attn_mx_, qkv_, 3L * D, qkv_ + D, qkv_ + 2L * D, 3L * D, cu_self_, Tl_, Bsa)) return 1;
   if (probe_sa && probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
-  if (!attn_mx_ && quant_rows_fp8(obuf_, D, Msa, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
-  if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa, 0, 0, Msa)) return 1;
+  if (f_proj) {
+    if (!attn_mx_ && quant_rows_fp8(obuf_, D, Msa, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
+    if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa, 0, 0, Msa)) return 1;
+  } else if (g16(obuf_, b.proj_w, D, nullptr, EPI_RESID_F32, x_, D, gate_sa, 0, 0, Msa)) {
+    return 1;
+  }
   for (long r0 = Msa; r0 < M_; r0 += Msa)  // the other CFG copies of the residual rows
     FLITE_HIP_CHECK(hipMemcpyAsync(x_ + r0 * D, x_, (size_t)Msa * D * sizeof(float), hipMemcpyDeviceToDevice, s));
   // --- cross attention --- (uniform-context collapse as in run_block: the first U sequences' rows take
   // x += gate_ca * c8, the rest run the sub-block from row r0 on)
-  const int U = b.cross ? uni_fp8() : 0;
+  // (an MXFP8 cross-q or cross-proj keeps the collapsed rows' r0 16-B aligned in the scale arrays: uni_fp8; a bf16
+  // cross-proj takes the bf16 path's c = V . Wproj^T)
+  const bool f_ca = f_cq || f_cproj;
+  const int U = b.cross ? (f_ca ? uni_fp8() : ctx_uni_) : 0;
   const long r0 = (long)U * Tl_, rows = M_ - r0;
-  if (U > 0 && ctx_bcast_resid(x_, ctx_c8_ + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s)) return 1;
+  if (U > 0 && ctx_bcast_resid(x_, (f_cproj ? ctx_c8_ : ctx_c_) + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s))
+    return 1;
   if (b.cross && rows > 0) {
-    if (norm8(b.norm2, shift_ca + U * mseg, scale_ca + U * mseg, rows, r0)) return 1;
-    if (g8(nbuf8_ + r0 * D, nbuf8_s_ + r0 * 4, q.cq, q.cq_s, D, D, D, b.cq_b,
-           fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16, qkv_ + r0 * D, D, nullptr, D, 0, rows))
+    if (f_cq ? norm8(b.norm2, shift_ca + U * mseg, scale_ca + U * mseg, rows, r0)
+             : norm16(b.norm2, shift_ca + U * mseg, scale_ca + U * mseg, rows, r0))
       return 1;
+    if (f_cq) {
+      if (g8(nbuf8_ + r0 * D, nbuf8_s_ + r0 * 4, q.cq, q.cq_s, D, D, D, b.cq_b,
+             fused ? EPI8_QKV_NORM_BF16 : EPI8_STORE_BF16, qkv_ + r0 * D, D, nullptr, D, 0, rows))
+        return 1;
+    } else if (g16(nbuf_ + r0 * D, b.cq_w, D, b.cq_b, fused ? EPI_QKV_NORM_BF16 : EPI_STORE_BF16, qkv_ + r0 * D, D,
+                   nullptr, D, 0, rows)) {
+      return 1;
+    }
     if (!fused && qk_norm(D, H, 0, rows, r0)) return 1;
-    if (attn(qkv_, D, ctx_kv_[blk], ctx_kv_[blk] + D, 2L * D, cu_ctx_ + U, ctx_max_len_, B_ - U, U)) return 1;
-    if (!attn_mx_ && quant_rows_fp8(obuf_ + r0 * D, D, rows, D, obuf8_ + r0 * D, D, obuf8_s_ + r0 * 4, mpad_, s))
+    if (attn(f_cproj && attn_mx_, qkv_, D, ctx_kv_[blk], ctx_kv_[blk] + D, 2L * D, cu_ctx_ + U, ctx_max_len_, B_ - U,
+             U))
       return 1;
-    if (g8(obuf8_ + r0 * D, obuf8_s_ + r0 * 4, q.cproj, q.cproj_s, D, D, D, nullptr, EPI8_RESID_F32, x_ + r0 * D, D,
-           gate_ca + U * mseg, 0, 0, rows))
+    if (f_cproj) {
+      if (!attn_mx_ && quant_rows_fp8(obuf_ + r0 * D, D, rows, D, obuf8_ + r0 * D, D, obuf8_s_ + r0 * 4, mpad_, s))
+        return 1;
+      if (g8(obuf8_ + r0 * D, obuf8_s_ + r0 * 4, q.cproj, q.cproj_s, D, D, D, nullptr, EPI8_RESID_F32, x_ + r0 * D, D,
+             gate_ca + U * mseg, 0, 0, rows))
+        return 1;
+    } else if (g16(obuf_ + r0 * D, b.cproj_w, D, nullptr, EPI_RESID_F32, x_ + r0 * D, D, gate_ca + U * mseg, 0, 0,
+                   rows)) {
       return 1;
+    }
   }
-  // --- SwiGLU MLP ---
-  if (norm8(b.norm3, shift_mlp, scale_mlp)) return 1;
+  // --- SwiGLU MLP --- (an fp8 gate/up writes the SwiGLU output as MXFP8 for an fp8 down, bf16 for a bf16 down; a
+  // bf16 gate/up feeding an fp8 down is quantised by quant_rows_fp8)
+  if (f_gu ? norm8(b.norm3, shift_mlp, scale_mlp) : norm16(b.norm3, shift_mlp, scale_mlp)) return 1;
   if (probe_begin(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
-  if (g8(nbuf8_, nbuf8_s_, q.gu, q.gu_s, 2L * F, 2 * F, D, nullptr, EPI8_SWIGLU_FP8, hbuf8_, F, nullptr)) return 1;
+  if (f_gu) {
+    if (f_down ? g8(nbuf8_, nbuf8_s_, q.gu, q.gu_s, 2L * F, 2 * F, D, nullptr, EPI8_SWIGLU_FP8, hbuf8_, F, nullptr)
+               : g8(nbuf8_, nbuf8_s_, q.gu, q.gu_s, 2L * F, 2 * F, D, nullptr, EPI8_SWIGLU_BF16, hbuf_, F, nullptr))
+      return 1;
+  } else {
+    GemmParams g;
+    g.A = nbuf_;
+    g.lda = D;
+    g.W = b.gate_w;
+    g.W2 = b.up_w;
+    g.ldw = D;
+    g.out = hbuf_;
+    g.ldo = F;
+    g.M = (int)M_;
+    g.N = 2 * F;
+    g.K = D;
+    if (gemm(g, EPI_SWIGLU_BF16, s)) return 1;
+    if (f_down && quant_rows_fp8(hbuf_, F, M_, F, hbuf8_, F, hbuf8_s_, mpad_, s)) return 1;
+  }
   if (probe_end(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
   if (probe_begin(s, FLITE_PROBE_GEMM_DOWN)) return 1;
-  if (g8(hbuf8_, hbuf8_s_, q.down, q.down_s, D, D, F, nullptr, EPI8_RESID_F32, x_, D, gate_mlp)) return 1;
+  if (f_down) {
+    if (g8(hbuf8_, hbuf8_s_, q.down, q.down_s, D, D, F, nullptr, EPI8_RESID_F32, x_, D, gate_mlp)) return 1;
+  } else {
+    GemmParams g;
+    g.A = hbuf_;
+    g.lda = F;
+    g.W = b.down_w;
+    g.ldw = F;
+    g.out = x_;
+    g.ldo = D;
+    g.gate = gate_mlp;
+    g.gate_seg_stride = mseg;
+    g.rows_per_seg = Tl_;
+    g.M = (int)M_;
+    g.N = D;
+    g.K = F;
+    if (gemm(g, EPI_RESID_F32, s)) return 1;
+  }
   if (probe_end(s, FLITE_PROBE_GEMM_DOWN)) return 1;
   return 0;
 }
@@ -1181,7 +1294,7 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     // cross-attention, so block 0's self-attention sub-block runs once per image instead of once per copy (one
     // rank; bf16 and MXFP8 paths)
     sa_seqs_ = (i == 0 && dup > 1 && t_row_step == 0 && sp_n_ == 1 && cfg_dedup()) ? Bi : 0;
-    const bool blk8 = fp8_ && !(i < (int)fp8_bf16_blk_.size() && fp8_bf16_blk_[i]);
+    const bool blk8 = fp8_ && fp8_classes_ != 0 && !(i < (int)fp8_bf16_blk_.size() && fp8_bf16_blk_[i]);
     const int rc = blk8 ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg);
     sa_seqs_ = 0;
     if (rc) return 1;

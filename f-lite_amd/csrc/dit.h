@@ -51,6 +51,7 @@ class DitEngine {
   // fp8 mode (flite_dit_enable_fp8): MXFP8 copies of the block GEMM weights + fp8 activations
   int enable_fp8(hipStream_t s, bool on);
   int set_fp8_bf16_blocks(const int* blocks, int n);
+  int set_fp8_classes(int mask);
   // the bound weights' CONTENTS changed in place (flite_dit_weights_updated): requantise the fp8 copies
   int weights_updated(hipStream_t s);
 
@@ -163,6 +164,7 @@ class DitEngine {
   };
   bool fp8_ = false;
   std::vector<char> fp8_bf16_blk_;  // blocks that stay bf16 in fp8 mode (flite_dit_set_fp8_bf16_blocks)
+  int fp8_classes_ = 63;            // GEMM classes on MXFP8 in the fp8 blocks (flite_dit_set_fp8_gemm_classes)
   bool w8_stale_ = true;  // the fp8 copies do not reflect the bound bf16 weights (requantised before the next use)
   bool ctx_stale_ = false;  // a weight changed after set_context: the cached context K/V are stale
   std::vector<Fp8W> w8_;

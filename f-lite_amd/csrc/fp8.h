@@ -32,6 +32,7 @@ enum GemmFp8Epilogue {
   EPI8_SWIGLU_FP8 = 4,  // W8 = gate|up interleaved in 16-row sub-tiles (N = 2F): out8[m][f] = MX(silu(g) * u),
                         // scales to out_sc [F/128][out_rows_pad][4]
   EPI8_QKV_NORM_BF16 = 5,  // engine-internal: bf16 store with RoPE + QK-norm of columns [0, norm_cols) (gemm.hip)
+  EPI8_SWIGLU_BF16 = 6,    // as EPI8_SWIGLU_FP8, out_bf16[m][f] = silu(g) * u (an fp8 gate/up feeding a bf16 down)
 };
 
 struct GemmFp8Params {

@@ -415,6 +415,27 @@ struct Fp8Cta {
         if (m < p.M && lk == 0) p.out_sc[((long)(blk >> 2) * p.out_rows_pad + m) * 4 + (blk & 3)] = (uint8_t)(e + 127);
       }
       return;
+    } else if constexpr (EPI == EPI8_SWIGLU_BF16) {
+      // the same gate/up pairs, h rounded to bf16: columns oc0 + 4 lk .. + 3 and oc0 + 16 + 4 lk .. + 3 of the row
+      const int F = p.N >> 1;
+      const int oc0 = (n0 >> 1) + wave_n * 32;
+      if (oc0 >= F) return;
+      bf16_t* ob = (bf16_t*)p.out;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int m = m_base + mi * 16;
+        float h[8];
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[4 * pr + r] = silu_f(acc[mi][2 * pr][r]) * acc[mi][2 * pr + 1][r];
+        if (m < p.M) {
+          bf16_t* orow = ob + (long)m * p.ldo + oc0 + lk * 4;
+          *(u32x2*)(orow) = u32x2{pack2bf(h[0], h[1]), pack2bf(h[2], h[3])};
+          *(u32x2*)(orow + 16) = u32x2{pack2bf(h[4], h[5]), pack2bf(h[6], h[7])};
+        }
+      }
+      return;
     } else if constexpr (EPI == EPI8_RESID_F32) {
       float bias[4][4];
       int nc[4];
@@ -539,6 +560,7 @@ int init8() {
   FLITE_HIP_CHECK(set_attrs8<EPI8_RESID_F32>());
   FLITE_HIP_CHECK(set_attrs8<EPI8_SWIGLU_FP8>());
   FLITE_HIP_CHECK(set_attrs8<EPI8_QKV_NORM_BF16>());
+  FLITE_HIP_CHECK(set_attrs8<EPI8_SWIGLU_BF16>());
   int dev = 0;
   FLITE_HIP_CHECK(hipGetDevice(&dev));
   FLITE_HIP_CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -613,6 +635,12 @@ int gemm_fp8(const GemmFp8Params& p, int epi, hipStream_t s) {
                     "gemm_fp8(swiglu): output scales / stride");
       FLITE_REQUIRE(p.bias == nullptr, "gemm_fp8(swiglu): no bias");
       launch8<EPI8_SWIGLU_FP8>(p, s);
+      break;
+    case EPI8_SWIGLU_BF16:
+      FLITE_REQUIRE(p.N % 256 == 0 && p.ldo % 4 == 0 && ((uintptr_t)p.out & 7) == 0,
+                    "gemm_fp8(swiglu bf16): 2F a multiple of 256, 8-B aligned rows");
+      FLITE_REQUIRE(p.bias == nullptr, "gemm_fp8(swiglu): no bias");
+      launch8<EPI8_SWIGLU_BF16>(p, s);
       break;
     case EPI8_QKV_NORM_BF16:
       FLITE_REQUIRE(p.N % 256 == 0 && p.ldo % 4 == 0 && p.norm_cols % 256 == 0 && p.rope_cols % 256 == 0 &&

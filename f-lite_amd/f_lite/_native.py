@@ -103,6 +103,7 @@ SIGNATURES = {
     "flite_rmsnorm_modulate_fp8": (_i, [_vp, _vp, _l, _vp, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
     "flite_dit_enable_fp8": (_i, [_vp, _vp, _i]),
     "flite_dit_set_fp8_bf16_blocks": (_i, [_vp, _vp, _i]),
+    "flite_dit_set_fp8_gemm_classes": (_i, [_vp, _i]),
     "flite_dit_weights_updated": (_i, [_vp, _vp]),
     "flite_vae_weights_updated": (_i, [_vp]),
     "flite_dit_set_sequence_parallel": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -219,6 +220,32 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias=None, *, out=None, epilogue=EPI_
     else:
         check(lib.flite_gemm_bf16(*args), "flite_gemm_bf16")
     return out
+
+
+# GEMM classes of the fp8 policy (include/flite.h FLITE_FP8_*)
+FP8_CLASSES = {"qkv": 1, "proj": 2, "cross_q": 4, "cross_proj": 8, "gate_up": 16, "down": 32}
+
+
+def fp8_class_mask(classes) -> int:
+    """An int mask, or an iterable of FP8_CLASSES names ("all" = every class)."""
+    if classes is None:
+        return 63
+    if isinstance(classes, int):
+        if not 0 <= classes <= 63:
+            raise FliteError(f"fp8 GEMM class mask {classes} outside 0..63")
+        return classes
+    if isinstance(classes, str):
+        classes = [c for c in classes.split(",") if c.strip()]
+    m = 0
+    for c in classes:
+        c = c.strip()
+        if c == "all":
+            m |= 63
+        elif c in FP8_CLASSES:
+            m |= FP8_CLASSES[c]
+        else:
+            raise FliteError(f"unknown fp8 GEMM class {c!r} (one of {sorted(FP8_CLASSES)} or 'all')")
+    return m
 
 
 def attn_workspace(device, batch, num_heads, max_q=0, max_k=0):
@@ -585,6 +612,10 @@ class DitEngine:
         blocks = [int(b) for b in blocks]
         arr = (ctypes.c_int * max(len(blocks), 1))(*blocks)
         check(self.lib.flite_dit_set_fp8_bf16_blocks(self.h, arr, len(blocks)), "flite_dit_set_fp8_bf16_blocks")
+
+    def set_fp8_gemm_classes(self, mask: int = 63):
+        """GEMM classes on MXFP8 in the fp8 blocks (include/flite.h flite_dit_set_fp8_gemm_classes)."""
+        check(self.lib.flite_dit_set_fp8_gemm_classes(self.h, int(mask)), "flite_dit_set_fp8_gemm_classes")
 
     def weights_updated(self, device=None):
         """The bound weights changed in place: remake the engine's derived copies (fp8: requantise)."""

@@ -327,15 +327,17 @@ class DiT(nn.Module):
         self._bound = (ptrs, vers)
         return self._engine
 
-    def enable_fp8(self, enabled: bool = True, bf16_blocks=()):
+    def enable_fp8(self, enabled: bool = True, bf16_blocks=(), gemm_classes=None):
         """BASELINE.json configs[4]: run every block GEMM (qkv, proj, cross q / proj, SwiGLU gate-up, down) on
         MXFP8 weights and activations (OCP e4m3, E8M0 scale per 32 K elements) on the gfx950 block-scaled MFMA.
-        The bf16 parameters stay the source of truth; the engine quantises them once. `bf16_blocks`: block indices
-        that keep their bf16 GEMMs (a precision policy, e.g. (0, depth - 1); DESIGN §4 prices each). No reference
-        counterpart (the reference runs bf16 only)."""
+        The bf16 parameters stay the source of truth; the engine quantises them once. Precision policies (DESIGN §5
+        prices each): `bf16_blocks`, block indices that keep their bf16 GEMMs (e.g. (0, depth - 1)); `gemm_classes`,
+        the GEMM classes that run MXFP8 in the other blocks (names of _native.FP8_CLASSES, e.g. ("gate_up",), or an
+        int mask; None = all). No reference counterpart (the reference runs bf16 only)."""
         self._fp8 = bool(enabled)
         eng = self.engine()
         eng.set_fp8_bf16_blocks(bf16_blocks)
+        eng.set_fp8_gemm_classes(_native.fp8_class_mask(gemm_classes))
         eng.enable_fp8(self._fp8, self.device)
         return self
 

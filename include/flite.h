@@ -295,6 +295,21 @@ int flite_dit_enable_fp8(flite_dit* dit, void* stream, int enable);
  */
 int flite_dit_set_fp8_bf16_blocks(flite_dit* dit, const int* blocks, int n);
 /*
+ * fp8 precision policy by GEMM class (round 5): in the fp8 blocks only the classes in `mask` run MXFP8, the others
+ * run their bf16 GEMMs on bf16 operands (each activation is produced in the format its consumer takes: the norm,
+ * the attention epilogue and the SwiGLU epilogue write bf16 or MXFP8 accordingly). Default FLITE_FP8_ALL. Classes:
+ * qkv (model.py:151), self-attention proj (:212), cross q (:196), cross proj (:212 of the cross block), SwiGLU
+ * gate|up (:261-267) and down (:267).
+ */
+#define FLITE_FP8_QKV 1
+#define FLITE_FP8_PROJ 2
+#define FLITE_FP8_CROSS_Q 4
+#define FLITE_FP8_CROSS_PROJ 8
+#define FLITE_FP8_GATE_UP 16
+#define FLITE_FP8_DOWN 32
+#define FLITE_FP8_ALL 63
+int flite_dit_set_fp8_gemm_classes(flite_dit* dit, int mask);
+/*
  * The CONTENTS of bound weights changed in place (a load_state_dict copy, a LoRA merge, re-initialisation):
  * every engine-owned copy derived from them is remade -- in fp8 mode the MXFP8 weights are requantised on
  * `stream` now. The bf16 path reads the bound storage directly. The cross-attention K/V cached by
