@@ -735,10 +735,6 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
   FLITE_REQUIRE(p.q_head_stride % 8 == 0 && p.k_head_stride % 8 == 0 && p.v_head_stride % 8 == 0,
                 "attention: head strides must be multiples of 8 elements");
   if (attn_init()) return 1;
-  {
-    const int r = attn_q256_fwd(p, stream);  // long bounded launches: 256 query rows per workgroup
-    if (r >= 0) return r;
-  }
   AttnParams q = p;
   q.n_main = (p.max_q + QT - 1) / QT;
   q.n_split = 0;
@@ -751,6 +747,10 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
   FLITE_REQUIRE(!p.o8 || (p.o8_scale && (p.part_mode == 0 || p.part_mode == 2) && p.o_row_stride % 128 == 0 && p.o_head_stride == HD &&
                           p.o8_rows_pad > 0),
                 "attention: MXFP8 output needs scales, 128-aligned rows and whole heads");
+  {
+    const int r = attn_q256_fwd(p, stream);  // long bounded launches: 256 query rows per workgroup
+    if (r >= 0) return r;
+  }
   if (p.part_mode == 0 && p.max_score > 0.f && p.split_ws != nullptr && p.max_q % QT != 0 &&
       pairs <= (int)(CNT_BYTES / 4) &&
       (p.max_k <= 0 || p.max_k >= MIN_SPLIT_KEYS)) {

@@ -31,6 +31,7 @@
 
 #include "attn_common.h"
 #include "common.h"
+#include "fp8.h"
 #include "kernels.h"
 
 namespace flite {
@@ -46,7 +47,9 @@ constexpr int TILE = KT * HD * 2;  // 16 KiB: one K or V tile
 // LDS: [K buf0 | K buf1 | V buf0 | V buf1]
 constexpr int K_OFF = 0;
 constexpr int V_OFF = 2 * TILE;
-constexpr int LDS_BYTES = 4 * TILE;  // 64 KiB
+// then [Q^T of query block 1: wave w at Q1_OFF + w * 16 KiB] (row-major 512-B rows, K's chunk swizzle)
+constexpr int Q1_OFF = 4 * TILE;
+constexpr int LDS_BYTES = 4 * TILE + 4 * 32 * 512;  // 128 KiB
 // slab: O^T accumulators lane-linear [wave 4][qb 2][dt 8][r4 4][lane 64] f32x4, then l [wave 4][qb 2][lane 64]
 constexpr int SLAB_O_F4 = 4 * 2 * 8 * 4 * 64;
 constexpr int SLAB_FLOATS = SLAB_O_F4 * 4 + 4 * 2 * 64;
@@ -129,20 +132,28 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
   }
   const int nt = t_end - t_begin;
 
-  // ---- Q^T fragments of both 32-row blocks, pre-scaled to log2 units (attention.hip: one bf16 rounding of q) ----
-  bf16x8 qf[32];  // [qb * 16 + k-step]
+  // ---- Q^T fragments of both 32-row blocks, pre-scaled to log2 units (attention.hip: one bf16 rounding of q).
+  // Block 0 stays in VGPRs (qf); block 1 goes to this wave's LDS region and is read back per k-step beside the K
+  // fragment (same row-major layout and swizzle as a K tile, so the same offsets): 64 VGPRs the key loop would
+  // otherwise not have (O takes all 256 AGPRs) for one extra ds_read_b128 per S MFMA pair ----
+  bf16x8 qf[16];
   {
     const float qs = p.scale * 1.4426950408889634f;
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 1; qb >= 0; --qb) {
       const int qc = min(q0 + wave * QW + qb * 32 + lq, q_len - 1);
       const bf16_t* qp = p.q + (long)(q_start + qc) * p.q_row_stride + (long)h * p.q_head_stride + 8 * hh;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) qf[qb * 16 + s] = *(const bf16x8*)(qp + 16 * s);
+      for (int s = 0; s < 16; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
 #pragma unroll
       for (int s = 0; s < 16; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qf[qb * 16 + s][j] = (__bf16)((float)qf[qb * 16 + s][j] * qs);
+        for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * qs);
+      if (qb == 1) {
+        char* q1w = smem + Q1_OFF + wave * 16384 + lq * 512;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) *(bf16x8*)(q1w + (s >> 3) * 256 + (((2 * (s & 7) + hh) ^ (lq & 15)) << 4)) = qf[s];
+      }
     }
   }
 
@@ -150,15 +161,16 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
   const long k_base = (long)k_start * p.k_row_stride + (long)h * p.k_head_stride;
   const long v_base = (long)k_start * p.v_row_stride + (long)h * p.v_head_stride;
   const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr_of(smem));
-  // per-lane source byte offsets of piece i, recomputed at each issue (3 VALU) rather than held in 8 registers
-  const int pos = lane & 31;
+  // Per-lane source byte offsets of piece i, and (below) the K fragment read offsets, are derived inside each phase A
+  // from an opaque copy of the lane index (`lane_a`): hipcc would otherwise hoist the 8 + 8 loop-invariant values
+  // into registers that stay allocated through phase B, where the register file is full (Q^T 128, S 32, P 32).
   const unsigned krow_b = (unsigned)(p.k_row_stride * 2), vrow_b = (unsigned)(p.v_row_stride * 2);
-  auto k_src = [&](int i) __attribute__((always_inline)) {
-    const int row = 2 * (wave * 4 + i) + hh;
+  auto k_src = [&](int i, int ln) __attribute__((always_inline)) {
+    const int row = 2 * (wave * 4 + i) + (ln >> 5), pos = ln & 31;
     return (unsigned)row * krow_b + (unsigned)((pos ^ (row & 15)) * 16);  // K: 16-B chunk XOR (row & 15)
   };
-  auto v_src = [&](int i) __attribute__((always_inline)) {
-    const int row = 2 * (wave * 4 + i) + hh;
+  auto v_src = [&](int i, int ln) __attribute__((always_inline)) {
+    const int row = 2 * (wave * 4 + i) + (ln >> 5), pos = ln & 31;
     return (unsigned)row * vrow_b + (unsigned)(((((pos >> 2) ^ (row & 3)) << 2) | (pos & 3)) * 16);  // V: 64-B XOR
   };
   const unsigned k_tile_b = (unsigned)(KT * p.k_row_stride * 2), v_tile_b = (unsigned)(KT * p.v_row_stride * 2);
@@ -184,11 +196,8 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
   float l_run[2] = {0.f, 0.f};
 
   // per-lane LDS read bases. K (A operand of S^T): row lq, k-step s reads chunk (2s + hh) ^ (lq & 15), i.e.
-  // (s >> 3) * 256 B + koff[s & 7] (the XOR leaves chunk bit 4 alone)
+  // (s >> 3) * 256 B + ((2 (s & 7) + hh) ^ (lq & 15)) * 16 (the XOR leaves chunk bit 4 alone)
   const char* kbase = smem + K_OFF + lq * 512;
-  int koff[8];
-#pragma unroll
-  for (int s = 0; s < 8; ++s) koff[s] = ((2 * s + hh) ^ (lq & 15)) << 4;
   // V (tr-read): group G = lane >> 4, li = lane & 15 -> row vq = li >> 2, 4-column piece vp = li & 3; d-tile dt at
   // (dt >> 2) * 256 B + voff[dt & 3]
   const int G = lane >> 4;
@@ -204,8 +213,8 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
   using I1 = std::integral_constant<int, 1>;
   using BT = std::integral_constant<bool, true>;
   using BF = std::integral_constant<bool, false>;
-  constexpr int KAHEAD = 1;  // K fragments read this many k-steps ahead (each feeds two MFMAs)
-  constexpr int VAHEAD = 1;  // V^T fragments read this many fragments (= 4 MFMAs) ahead
+  constexpr int KAHEAD = 2;  // K (+ block-1 Q) fragments read this many k-steps ahead
+  constexpr int VAHEAD = 2;  // V^T fragments read this many fragments (= 4 MFMAs) ahead
   f32x16 s0, s1;             // S^T of the pending tile: query block 0 / 1
   u32x4 pa[4], pb[4];        // P^T operands [qb * 2 + 16-key step] of two consecutive tiles, bf16 pairs
 
@@ -219,8 +228,16 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
       krs = rsrc_tile(k_ptr0, k_tile_b, k_total_b, tk, k_on);
       vrs = rsrc_tile(v_ptr0, v_tile_b, v_total_b, tv, v_on);
     }
-    bf16x8 kf[16];
-    auto rdk = [&](int s) __attribute__((always_inline)) { kf[s] = *(const bf16x8*)(Kb + (s >> 3) * 256 + koff[s & 7]); };
+    int lane_a = lane;
+    asm volatile("" : "+v"(lane_a));  // opaque per phase: the offsets below are not hoisted out of the key loop
+    const int kx = lane_a & 15, kh = lane_a >> 5;
+    const char* Q1 = smem + Q1_OFF + wave * 16384 + (lane_a & 31) * 512;
+    bf16x8 kf[16], q1[16];
+    auto rdk = [&](int s) __attribute__((always_inline)) {
+      const int off = (s >> 3) * 256 + (((2 * (s & 7) + kh) ^ kx) << 4);
+      kf[s] = *(const bf16x8*)(Kb + off);
+      q1[s] = *(const bf16x8*)(Q1 + off);
+    };
     if constexpr (LIVE) {
 #pragma unroll
       for (int s = 0; s < KAHEAD; ++s) rdk(s);
@@ -233,10 +250,10 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
         __builtin_amdgcn_sched_barrier(0);
         if (s == 0) {
           mfma_sv_first(s0, kf[0], qf[0]);
-          mfma_sv_first(s1, kf[0], qf[16]);
+          mfma_sv_first(s1, kf[0], q1[0]);
         } else {
           mfma_sv(s0, kf[s], qf[s]);
-          mfma_sv(s1, kf[s], qf[16 + s]);
+          mfma_sv(s1, kf[s], q1[s]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -244,14 +261,16 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
         if ((s & 1) == 0) {
           const int i = s >> 1;
           if (i < 4)
-            blds16(krs, k_src(i), lds0 + DKB * TILE + (wave * 4 + i) * 1024 + K_OFF);
+            blds16(krs, k_src(i, lane_a), lds0 + DKB * TILE + (wave * 4 + i) * 1024 + K_OFF);
           else
-            blds16(vrs, v_src(i - 4), lds0 + DVB * TILE + (wave * 4 + i - 4) * 1024 + V_OFF);
+            blds16(vrs, v_src(i - 4, lane_a), lds0 + DVB * TILE + (wave * 4 + i - 4) * 1024 + V_OFF);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (LIVE) mfma_read_fence(s0, s1);  // MFMA write of S -> VALU read (softmax in the next phase B)
+    if constexpr (LIVE) {
+      mfma_read_fence(s0, s1);  // MFMA write of S -> VALU read (softmax in the next phase B)
+    }
   };
   // softmax of score e (0..31: block e >> 4, register r = e & 15) of the pending S into the P^T operand pn; the row
   // sum adds the PREVIOUS score's p (same adds, same order; no v_add waiting on the v_exp just issued)
@@ -288,32 +307,38 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
       __builtin_amdgcn_sched_barrier(0);
       const s16x8 c = __builtin_shufflevector(lo[f], hi[f], 0, 1, 2, 3, 4, 5, 6, 7);
       const bf16x8 vf = __builtin_bit_cast(bf16x8, c);
-      // P was packed a whole phase A earlier (no VALU -> MFMA hazard left to clear), and it is read in place: the
-      // NOP form's "+v" operand made hipcc copy each block's P into one register set right behind the previous
-      // MFMA reading it (v_mov_b64 + s_nop 1), which returned the other block's P for the second MFMA
+      // P was packed a whole phase A earlier (no VALU -> MFMA hazard left to clear), so it is read in place: the NOP
+      // form's "+v" operand would make hipcc copy each block's P into a scratch register set before every group
       bf16x8 pk = __builtin_bit_cast(bf16x8, pc[qb * 2 + s]);
       mfma_o<false>(o_acc[qb * 8 + dt], vf, pk);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (EX) softmax_elem(pn, m, e_prev);
       __builtin_amdgcn_sched_barrier(0);
-    }
+    }  // the P operands of the last two MFMAs
     if constexpr (EX) l_run[1] += e_prev;
   };
   // iteration j (parity PAR): phase A for S_{j+1} (HS) and phase B for PV_j with the softmax of S_{j+1}
-  auto iter = [&](auto par_, auto hs_, auto live_, int j) __attribute__((always_inline)) {
+  // Every iteration runs both phases, also past the last tile (phase A then computes the S of a tile past the range
+  // from zero-filled copies, and its softmax is kept out of the row sums): one code path for every tile. A remainder
+  // iteration outside the loop had its own register assignment, and there hipcc moved O accumulators through AGPR
+  // copies (v_accvgpr_write / mov) right before the asm MFMAs reading them, a VALU -> MFMA hazard it cannot see
+  // through the asm (measured: wrong d-tiles of block 1 in the last tile); a mid-loop exit spilled O to scratch.
+  auto iter = [&](auto par_, auto live_, int j) __attribute__((always_inline)) {
     constexpr int PAR = decltype(par_)::value;
-    constexpr bool HS = decltype(hs_)::value, LIVE = decltype(live_)::value;
-    if constexpr (HS) {
-      if constexpr (PAR == 0)
-        phase_a(I1{}, I0{}, I1{}, BT{}, live_, t_begin + j + 2, j + 2 < nt, t_begin + j + 1, true);
-      else
-        phase_a(I0{}, I1{}, I0{}, BT{}, live_, t_begin + j + 2, j + 2 < nt, t_begin + j + 1, true);
-    }
+    constexpr bool LIVE = decltype(live_)::value;
+    const bool next = j + 1 < nt;  // the tile whose S phase A computes exists
+    if constexpr (PAR == 0)
+      phase_a(I1{}, I0{}, I1{}, BT{}, live_, t_begin + j + 2, j + 2 < nt, t_begin + j + 1, next);
+    else
+      phase_a(I0{}, I1{}, I0{}, BT{}, live_, t_begin + j + 2, j + 2 < nt, t_begin + j + 1, next);
     if constexpr (LIVE) {
+      const float l0 = l_run[0], l1 = l_run[1];
       if constexpr (PAR == 0)
-        phase_b(I0{}, hs_, pa, pb);
+        phase_b(I0{}, BT{}, pa, pb);
       else
-        phase_b(I1{}, hs_, pb, pa);
+        phase_b(I1{}, BT{}, pb, pa);
+      l_run[0] = next ? l_run[0] : l0;
+      l_run[1] = next ? l_run[1] : l1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -327,9 +352,9 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
       const i32x4 krs1 = rsrc_tile(k_ptr0, k_tile_b, k_total_b, t_begin + 1, nt > 1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        blds16(krs, k_src(i), lds0 + (wave * 4 + i) * 1024 + K_OFF);
-        blds16(vrs, v_src(i), lds0 + (wave * 4 + i) * 1024 + V_OFF);
-        blds16(krs1, k_src(i), lds0 + TILE + (wave * 4 + i) * 1024 + K_OFF);
+        blds16(krs, k_src(i, lane), lds0 + (wave * 4 + i) * 1024 + K_OFF);
+        blds16(vrs, v_src(i, lane), lds0 + (wave * 4 + i) * 1024 + V_OFF);
+        blds16(krs1, k_src(i, lane), lds0 + TILE + (wave * 4 + i) * 1024 + K_OFF);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -343,15 +368,11 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
     }
     __syncthreads();  // every wave's K_0 reads are done before iteration 0 refills Kbuf 0
     int j = 0;
-    for (; j + 2 < nt; j += 2) {
-      iter(I0{}, BT{}, live_, j);
-      iter(I1{}, BT{}, live_, j + 1);
-    }
-    if (nt - j == 2) {
-      iter(I0{}, BT{}, live_, j);
-      iter(I1{}, BF{}, live_, j + 1);
-    } else {
-      iter(I0{}, BF{}, live_, j);
+    // tiles in pairs, one exit: with nt odd the last pair's second tile is a ghost whose V copy was staged as zeros
+    // (v_on false), so its PV adds exact zeros to O, and whose softmax was kept out of the row sums
+    for (; j < nt; j += 2) {
+      iter(I0{}, live_, j);
+      iter(I1{}, live_, j + 1);
     }
   };
   if (nt > 0) {
@@ -469,12 +490,85 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
         st.y = pack2bf(acc[2] * inv, acc[3] * inv);
         *(u32x2*)(p.o + (long)(q_start + row) * p.o_row_stride + (long)h * p.o_head_stride + d) = st;
       }
+      if (p.o8) {  // the tail rows' MXFP8 copy, from the bf16 rows this workgroup just stored (as attention.hip)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int t = tid; t < rows * 8; t += NT) {
+          const int row = q0 + (t >> 3), i = t & 7;
+          const long grow = q_start + row;
+          const u32x4* src = (const u32x4*)(p.o + grow * p.o_row_stride + (long)h * p.o_head_stride + i * 32);
+          float x[32];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const u32x4 w = src[q];
+            const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              x[8 * q + 2 * j] = __uint_as_float(ws[j] << 16);
+              x[8 * q + 2 * j + 1] = __uint_as_float(ws[j] & 0xffff0000u);
+            }
+          }
+          float amax = 0.f;
+#pragma unroll
+          for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(x[j]));
+          const int e = mx_exp(amax);
+          const float is = mx_inv(e);
+          u32x4 o[2];
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf)
+            o[hf] = u32x4{pack4_fp8(x + 16 * hf, is), pack4_fp8(x + 16 * hf + 4, is), pack4_fp8(x + 16 * hf + 8, is),
+                          pack4_fp8(x + 16 * hf + 12, is)};
+          u32x4* dst = (u32x4*)(p.o8 + grow * p.o_row_stride + (long)h * p.o_head_stride + i * 32);
+          dst[0] = o[0];
+          dst[1] = o[1];
+          const long kb = (long)h * (HD / 32) + i;
+          p.o8_scale[((kb >> 2) * p.o8_rows_pad + grow) * 4 + (kb & 3)] = (uint8_t)(e + 127);
+        }
+      }
       return;
     }
   }
 
   // ---- store: lane (row, hh) holds columns i*32 + 8*r4 + 4*hh + 0..3 of its row (attention.hip's epilogue) ----
   if (!live) return;
+  if (p.o8) {  // MXFP8 straight from the accumulators (the fp8 DiT's proj operand; attention.hip's o8 epilogue)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q_row = q0 + wave * QW + qb * 32 + lq;
+      const bool ok = q_row < q_len;
+      const float inv = l_run[qb] > 0.f ? 1.f / l_run[qb] : 0.f;
+      const long grow = q_start + min(q_row, q_len - 1);
+      uint8_t* o8row = p.o8 + grow * p.o_row_stride + (long)h * p.o_head_stride;
+      unsigned sc_lo = 0, sc_hi = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float x[16];
+        float amax = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          x[r] = bf2f(f2bf(o_acc[qb * 8 + i][r] * inv));  // the bf16 value quant_rows_fp8 would have read
+          amax = fmaxf(amax, fabsf(x[r]));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        const int e = mx_exp(amax);
+        const float is = mx_inv(e);
+        unsigned d[4];
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) d[r4] = pack4_fp8(x + 4 * r4, is);  // columns 8 r4 + 4 hh + 0..3
+#pragma unroll
+        for (int rp = 0; rp < 2; ++rp) {
+          const auto w = __builtin_amdgcn_permlane32_swap(d[2 * rp], d[2 * rp + 1], false, false);
+          if (ok) *(u32x2*)(o8row + i * 32 + 16 * rp + 8 * hh) = u32x2{w[0], w[1]};
+        }
+        const unsigned byte = (unsigned)(e + 127) << (8 * (i & 3));
+        if (i < 4) sc_lo |= byte; else sc_hi |= byte;
+      }
+      const long kt = (long)h * (HD / 128) + hh;  // the row's 8 block scales of this head: two 128-deep k-tiles
+      if (ok) *(unsigned*)(p.o8_scale + (kt * p.o8_rows_pad + grow) * 4) = hh ? sc_hi : sc_lo;
+    }
+    return;
+  }
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const int q_row = q0 + wave * QW + qb * 32 + lq;
@@ -559,6 +653,9 @@ Plan make_plan(int cus, int pairs, int max_q, int max_k) {
     }
   }
   pl.ws_bytes = CNT_BYTES + ((long)pl.n_half * 2 + (long)pairs * pl.n_tail) * SLAB_BYTES;
+  if (getenv("FLITE_Q256_VERBOSE"))
+    fprintf(stderr, "[q256] pairs %d max_q %d max_k %d: %d whole + %d split tiles, %d tail chunks (sim %.1f tiles)\n",
+            pairs, max_q, max_k, pl.n_whole, pl.n_half, pl.n_tail, best);
   return pl;
 }
 
@@ -576,8 +673,10 @@ int q256_init() {
   int dev = 0;
   FLITE_HIP_CHECK(hipGetDevice(&dev));
   FLITE_HIP_CHECK(hipDeviceGetAttribute(&g_q256_cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const char* off = getenv("FLITE_NO_ATTN_Q256");  // A/B switch: every attention on the 128-row kernel
-  g_q256_off = off && off[0] == '1';
+  // policy: the 256-row route is opt-in while it does not beat the 128-row kernel on the DiT shapes:
+  // FLITE_ATTN_Q256=1, or flite_attn_set_q256(1)
+  const char* on = getenv("FLITE_ATTN_Q256");
+  g_q256_off = !(on && on[0] == '1');
   if (const char* mk = getenv("FLITE_Q256_MIN_KEYS")) g_min_keys = std::max(KT, atoi(mk));  // A/B: key-range floor
   g_q256_attr = true;
   return 0;
@@ -594,9 +693,15 @@ const Plan* plan_for(int pairs, int max_q, int max_k) {
 
 }  // namespace
 
+int attn_q256_set(int on) {
+  if (q256_init()) return 1;
+  g_q256_off = !on;
+  return 0;
+}
+
 bool attn_q256_eligible(const AttnParams& p) {
   if (q256_init() || g_q256_off) return false;
-  return p.head_dim == HD && p.max_score > 0.f && p.part_mode == 0 && !p.o8 && !p.k_end && p.split_ws &&
+  return p.head_dim == HD && p.max_score > 0.f && p.part_mode == 0 && !p.k_end && p.split_ws &&
          p.max_q >= QT && p.max_k >= g_min_keys && p.B * p.H * (p.max_q / QT) <= (int)(CNT_BYTES / 4) - p.B * p.H;
 }
 

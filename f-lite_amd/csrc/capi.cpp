@@ -105,6 +105,8 @@ int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void
 
 long flite_attn_workspace_bytes(int batch, int num_heads) { return attn_split_workspace_bytes(batch, num_heads); }
 
+int flite_attn_set_q256(int enable) { return attn_q256_set(enable != 0); }
+
 long flite_attn_workspace_bytes_for(int batch, int num_heads, int max_seqlen_q, int max_seqlen_k) {
   if (batch <= 0 || num_heads <= 0 || max_seqlen_q < 0 || max_seqlen_k < 0) return 0;
   return attn_workspace_bytes(batch, num_heads, max_seqlen_q, max_seqlen_k);

@@ -60,6 +60,7 @@ SIGNATURES = {
     "flite_attn_varlen_fwd": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _f, _f]),
     "flite_attn_workspace_bytes": (_l, [_i, _i]),
     "flite_attn_workspace_bytes_for": (_l, [_i, _i, _i, _i]),
+    "flite_attn_set_q256": (_i, [_i]),
     "flite_attn_varlen_fwd_ws": (_i, [_vp, _vp, _vp, _vp, _vp, _l, _l, _l, _l, _l, _vp, _vp, _i, _i, _i, _i, _i, _f,
                                       _f, _vp, _l]),
     "flite_rmsnorm_modulate": (_i, [_vp, _vp, _i, _l, _vp, _l, _vp, _vp, _vp, _l, _l, _l, _i, _f]),
@@ -257,6 +258,11 @@ def attn_workspace(device, batch, num_heads, max_q=0, max_k=0):
     else:
         n = int(load().flite_attn_workspace_bytes(batch, num_heads))
     return torch.zeros(n, dtype=torch.uint8, device=device) if n > 0 else None
+
+
+def attn_set_q256(enable: bool):
+    """Route long bounded launches to the 256-query-row kernel (process-wide; include/flite.h flite_attn_set_q256)."""
+    check(load().flite_attn_set_q256(int(bool(enable))), "flite_attn_set_q256")
 
 
 def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None, max_score=0.0, workspace=None, max_k=0):

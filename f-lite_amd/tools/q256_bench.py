@@ -19,16 +19,22 @@ import torch  # noqa: E402
 
 from f_lite import _native as nat  # noqa: E402
 
+nat.attn_set_q256(True)
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--shapes", default="self,self1344,cross", help="comma list of: self, self1344, cross, round")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     D = 256
-    shapes = [("self 1024^2", [4112, 4112], [4112, 4112], 12), ("self 1344x896", [4720, 4720], [4720, 4720], 12),
-              ("cross cond-only", [4112], [512], 12)]
+    known = {"self": ("self 1024^2", [4112, 4112], [4112, 4112], 12),
+             "self1344": ("self 1344x896", [4720, 4720], [4720, 4720], 12),
+             "cross": ("cross cond-only", [4112], [512], 12),
+             "round": ("one round 2x4096 H8", [4096, 4096], [4096, 4096], 8)}  # 256 q256 tiles = 1 round, no tail
+    shapes = [known[s] for s in args.shapes.split(",")]
     g = torch.Generator(device=dev).manual_seed(3)
 
     def unit(x):

@@ -17,6 +17,8 @@ import torch  # noqa: E402
 
 from f_lite import _native as nat  # noqa: E402
 
+nat.attn_set_q256(True)
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -47,6 +49,15 @@ def main():
             qq, kk, vv = q[s0:s1, h].float(), k[s0:s1, h].float(), v[s0:s1, h].float()
             ref[s0:s1, h] = torch.softmax(qq @ kk.T / 16.0, -1) @ vv
     print(f"counters after the q256 launch: {cnt} (0 = reset)")
+    # rows of query block 1 vs block 0 of each wave in the first tile of (0, 0) (variant builds that feed block 1 the
+    # block-0 queries must give equal rows)
+    t = new[:256, 0].view(4, 2, 32, D)
+    print("qb1 - qb0 max |diff| per wave:", [float((t[w, 1] - t[w, 0]).abs().max()) for w in range(4)])
+    for row in (0, 33, 40, 63, 97):  # per 32-column block: relative error and the least-squares scale out/ref
+        o, r_ = new[row, 0], ref[row, 0]
+        blk = [(round(float((o[c:c + 32] - r_[c:c + 32]).norm() / r_[c:c + 32].norm()), 3),
+                round(float((o[c:c + 32] * r_[c:c + 32]).sum() / (r_[c:c + 32] ** 2).sum()), 3)) for c in range(0, 256, 32)]
+        print(f"row {row}: per d-tile (rel err, scale): {blk}")
     for name, out in (("q256", new), ("q128", old)):
         bad = []
         for b in range(B):

@@ -89,6 +89,8 @@ long flite_attn_workspace_bytes(int batch, int num_heads);
  * >= flite_attn_workspace_bytes(batch, num_heads).
  */
 long flite_attn_workspace_bytes_for(int batch, int num_heads, int max_seqlen_q, int max_seqlen_k);
+/* Process-wide switch of that 256-query-row route (default off unless FLITE_ATTN_Q256=1 in the environment). */
+int flite_attn_set_q256(int enable);
 
 /*
  * flite_attn_varlen_fwd with a caller-owned split workspace (device memory, zero-filled once, left zeroed by

@@ -374,7 +374,12 @@ def test_attention_q256(lens_q, lens_k, H):
     k = R.own_rmsnorm(torch.randn(int(cu_k[-1]), H, D, device=DEV, generator=g), None).bfloat16()
     v = torch.randn(int(cu_k[-1]), H, D, device=DEV, generator=g).bfloat16()
     args = (q, k, v, cu_q.to(DEV), cu_k.to(DEV), max(lens_q), D ** -0.5)
-    new = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
+    nat.attn_set_q256(True)
+    try:
+        new = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
+        again = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
+    finally:
+        nat.attn_set_q256(False)
     assert int(ws[:16384].view(torch.int32).abs().sum().item()) == 0  # counters left zeroed
     old = nat.attn_varlen(*args, max_score=16.5, workspace=ws)  # no max_k: the 128-row kernel
     assert torch.isfinite(new.float()).all()
@@ -386,5 +391,4 @@ def test_attention_q256(lens_q, lens_k, H):
     assert rel(new, ref) < 1e-2
     print(f"q256 {lens_q} x {lens_k} H={H}: rel vs fp32 {rel(new, ref):.2e} (128-row kernel {rel(old, ref):.2e})")
     assert rel(new, old) < 5e-3  # same math; split halves and chunk sums change the summation order only
-    again = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
     assert torch.equal(new, again)  # deterministic whichever split piece arrives last
