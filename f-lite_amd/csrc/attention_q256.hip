@@ -47,9 +47,7 @@ constexpr int TILE = KT * HD * 2;  // 16 KiB: one K or V tile
 // LDS: [K buf0 | K buf1 | V buf0 | V buf1]
 constexpr int K_OFF = 0;
 constexpr int V_OFF = 2 * TILE;
-// then [Q^T of query block 1: wave w at Q1_OFF + w * 16 KiB] (row-major 512-B rows, K's chunk swizzle)
-constexpr int Q1_OFF = 4 * TILE;
-constexpr int LDS_BYTES = 4 * TILE + 4 * 32 * 512;  // 128 KiB
+constexpr int LDS_BYTES = 4 * TILE;  // 64 KiB
 // slab: O^T accumulators lane-linear [wave 4][qb 2][dt 8][r4 4][lane 64] f32x4, then l [wave 4][qb 2][lane 64]
 constexpr int SLAB_O_F4 = 4 * 2 * 8 * 4 * 64;
 constexpr int SLAB_FLOATS = SLAB_O_F4 * 4 + 4 * 2 * 64;
@@ -132,28 +130,22 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
   }
   const int nt = t_end - t_begin;
 
-  // ---- Q^T fragments of both 32-row blocks, pre-scaled to log2 units (attention.hip: one bf16 rounding of q).
-  // Block 0 stays in VGPRs (qf); block 1 goes to this wave's LDS region and is read back per k-step beside the K
-  // fragment (same row-major layout and swizzle as a K tile, so the same offsets): 64 VGPRs the key loop would
-  // otherwise not have (O takes all 256 AGPRs) for one extra ds_read_b128 per S MFMA pair ----
-  bf16x8 qf[16];
+  // ---- Q^T fragments of both 32-row blocks in VGPRs (128), pre-scaled to log2 units (attention.hip: one bf16
+  // rounding of q). Measured alternative: block 1 kept in LDS and read beside each K fragment frees 64 VGPRs but
+  // made phase A LDS-read-bound (2 x 4096 x 4096, H 8: 236.5 vs 222.1 us) ----
+  bf16x8 qf[32];
   {
     const float qs = p.scale * 1.4426950408889634f;
 #pragma unroll
-    for (int qb = 1; qb >= 0; --qb) {
+    for (int qb = 0; qb < 2; ++qb) {
       const int qc = min(q0 + wave * QW + qb * 32 + lq, q_len - 1);
       const bf16_t* qp = p.q + (long)(q_start + qc) * p.q_row_stride + (long)h * p.q_head_stride + 8 * hh;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) qf[s] = *(const bf16x8*)(qp + 16 * s);
+      for (int s = 0; s < 16; ++s) qf[qb * 16 + s] = *(const bf16x8*)(qp + 16 * s);
 #pragma unroll
       for (int s = 0; s < 16; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qf[s][j] = (__bf16)((float)qf[s][j] * qs);
-      if (qb == 1) {
-        char* q1w = smem + Q1_OFF + wave * 16384 + lq * 512;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) *(bf16x8*)(q1w + (s >> 3) * 256 + (((2 * (s & 7) + hh) ^ (lq & 15)) << 4)) = qf[s];
-      }
+        for (int j = 0; j < 8; ++j) qf[qb * 16 + s][j] = (__bf16)((float)qf[qb * 16 + s][j] * qs);
     }
   }
 
@@ -231,12 +223,10 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
     int lane_a = lane;
     asm volatile("" : "+v"(lane_a));  // opaque per phase: the offsets below are not hoisted out of the key loop
     const int kx = lane_a & 15, kh = lane_a >> 5;
-    const char* Q1 = smem + Q1_OFF + wave * 16384 + (lane_a & 31) * 512;
-    bf16x8 kf[16], q1[16];
+    bf16x8 kf[16];
     auto rdk = [&](int s) __attribute__((always_inline)) {
       const int off = (s >> 3) * 256 + (((2 * (s & 7) + kh) ^ kx) << 4);
       kf[s] = *(const bf16x8*)(Kb + off);
-      q1[s] = *(const bf16x8*)(Q1 + off);
     };
     if constexpr (LIVE) {
 #pragma unroll
@@ -250,10 +240,10 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
         __builtin_amdgcn_sched_barrier(0);
         if (s == 0) {
           mfma_sv_first(s0, kf[0], qf[0]);
-          mfma_sv_first(s1, kf[0], q1[0]);
+          mfma_sv_first(s1, kf[0], qf[16]);
         } else {
           mfma_sv(s0, kf[s], qf[s]);
-          mfma_sv(s1, kf[s], q1[s]);
+          mfma_sv(s1, kf[s], qf[16 + s]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -597,6 +587,8 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
 struct Plan {
   int n_whole = 0, n_half = 0, n_tail = 0;
   long ws_bytes = 0;
+  bool wins = false;  // predicted faster than the 128-row kernel's schedule (route policy)
+  double t256 = 0, t128 = 0;
 };
 
 // Makespan of the item list on `cus` CUs when each CU takes the next item as it frees (the dispatcher, to first
@@ -611,14 +603,40 @@ double simulate(int cus, int n_whole, int n_half, int pairs, int n_tail, int nk,
     q.push(t);
     end = std::max(end, t);
   };
-  const double pro = 4.0;
-  for (int i = 0; i < n_whole; ++i) run(nk + pro);
+  // a 32-key iteration of this kernel costs 0.96 of a 64-key iteration of the 128-row kernel (the same MFMA work;
+  // measured 222.1 vs 231.8 us on 2 x 4096 x 4096, H 8, one round of each); the prologue (the Q burst) ~6
+  const double it = 0.96, pro = 6.0;
+  for (int i = 0; i < n_whole; ++i) run(it * (nk + (nk & 1)) + pro);  // an odd count runs one ghost iteration
   const int half = (nk + 1) / 2;
-  for (int i = 0; i < 2 * n_half; ++i) run(half + pro + 1.0);
+  for (int i = 0; i < 2 * n_half; ++i) run(it * (half + (half & 1)) + pro + 2.0);  // + the slab hand-off
   if (n_tail > 0) {
     const int per = (nk + n_tail - 1) / n_tail;
     const double live = (tail_rows + QW - 1) / QW;  // live waves: MFMA work of the chunk relative to a full tile
-    for (int i = 0; i < pairs * n_tail; ++i) run(per * std::max(0.35, live / 4.0) + 3.0 + 0.5 * n_tail / 4.0);
+    for (int i = 0; i < pairs * n_tail; ++i)
+      run(it * (per + (per & 1)) * std::max(0.35, live / 4.0) + pro * 0.5 + 0.5 * n_tail / 4.0);
+  }
+  return end;
+}
+
+// The 128-row kernel's schedule (attention.hip attn_fwd) in the same units: full 128-row q-tiles over every 64-key
+// tile, then the tail chunks (min(CUs / pairs, 16) key ranges per pair)
+double simulate128(int cus, int pairs, int max_q, int max_k) {
+  std::priority_queue<double, std::vector<double>, std::greater<double>> q;
+  for (int i = 0; i < cus; ++i) q.push(0.0);
+  double end = 0.0;
+  auto run = [&](double c) {
+    const double t = q.top() + c;
+    q.pop();
+    q.push(t);
+    end = std::max(end, t);
+  };
+  const int nk = (max_k + 63) / 64, n_main = max_q / 128, tail = max_q - 128 * n_main;
+  const double pro = 4.0;
+  for (int i = 0; i < pairs * n_main; ++i) run(nk + pro);
+  if (tail > 0) {
+    const int S = std::max(1, std::min(cus / pairs, 16));
+    const int per = (nk + S - 1) / S;
+    for (int i = 0; i < pairs * S; ++i) run(per + pro * 0.5 + 0.5 * S / 4.0);
   }
   return end;
 }
@@ -653,9 +671,15 @@ Plan make_plan(int cus, int pairs, int max_q, int max_k) {
     }
   }
   pl.ws_bytes = CNT_BYTES + ((long)pl.n_half * 2 + (long)pairs * pl.n_tail) * SLAB_BYTES;
+  pl.t256 = simulate(cus, pl.n_whole, pl.n_half, pairs, pl.n_tail, nk, tail_rows);
+  pl.t128 = simulate128(cus, pairs, max_q, max_k);
+  // margin 4.5 %: measured against the prediction (2 x T self-attention, 12 heads): T = 4720 predicted 0.949, measured
+  // 473 vs 505 us (taken); T = 4112 predicted 0.972, 405 vs 384 us; T = 9232 predicted 0.960, 1856 vs 1783 us
+  pl.wins = pl.t256 < 0.955 * pl.t128;
   if (getenv("FLITE_Q256_VERBOSE"))
-    fprintf(stderr, "[q256] pairs %d max_q %d max_k %d: %d whole + %d split tiles, %d tail chunks (sim %.1f tiles)\n",
-            pairs, max_q, max_k, pl.n_whole, pl.n_half, pl.n_tail, best);
+    fprintf(stderr, "[q256] pairs %d max_q %d max_k %d: %d whole + %d split tiles, %d tail chunks; predicted %.1f vs "
+            "%.1f (128-row kernel): %s\n", pairs, max_q, max_k, pl.n_whole, pl.n_half, pl.n_tail, pl.t256, pl.t128,
+            pl.wins ? "256-row" : "128-row");
   return pl;
 }
 
@@ -663,7 +687,7 @@ std::mutex g_plan_mu;
 std::map<std::tuple<int, int, int, int>, Plan> g_plans;
 bool g_q256_attr = false;
 int g_q256_cus = 0;
-int g_q256_off = -1;
+int g_q256_mode = 2;  // 0 never, 1 always, 2 by the plan's prediction
 int g_min_keys = MIN_KEYS;
 
 int q256_init() {
@@ -673,10 +697,12 @@ int q256_init() {
   int dev = 0;
   FLITE_HIP_CHECK(hipGetDevice(&dev));
   FLITE_HIP_CHECK(hipDeviceGetAttribute(&g_q256_cus, hipDeviceAttributeMultiprocessorCount, dev));
-  // policy: the 256-row route is opt-in while it does not beat the 128-row kernel on the DiT shapes:
-  // FLITE_ATTN_Q256=1, or flite_attn_set_q256(1)
+  // route policy: by default a launch takes the 256-row kernel where its split plan is predicted >= 4.5 %
+  // faster than the 128-row kernel's schedule (the 1344x896 self-attention, T = 4720: 465 vs 495 us measured; not
+  // at 1024^2, T = 4112, whose 768 128-row q-tiles are exactly 3 rounds of 256 CUs: 401 vs 375 us). FLITE_ATTN_Q256=1
+  // / 0 or flite_attn_set_q256(1 / 0): always / never (the tests and A/B tools)
   const char* on = getenv("FLITE_ATTN_Q256");
-  g_q256_off = !(on && on[0] == '1');
+  g_q256_mode = !on ? 2 : on[0] == '1' ? 1 : 0;
   if (const char* mk = getenv("FLITE_Q256_MIN_KEYS")) g_min_keys = std::max(KT, atoi(mk));  // A/B: key-range floor
   g_q256_attr = true;
   return 0;
@@ -693,14 +719,14 @@ const Plan* plan_for(int pairs, int max_q, int max_k) {
 
 }  // namespace
 
-int attn_q256_set(int on) {
+int attn_q256_set(int mode) {
   if (q256_init()) return 1;
-  g_q256_off = !on;
+  g_q256_mode = mode < 0 ? 0 : mode > 2 ? 2 : mode;
   return 0;
 }
 
 bool attn_q256_eligible(const AttnParams& p) {
-  if (q256_init() || g_q256_off) return false;
+  if (q256_init() || g_q256_mode == 0) return false;
   return p.head_dim == HD && p.max_score > 0.f && p.part_mode == 0 && !p.k_end && p.split_ws &&
          p.max_q >= QT && p.max_k >= g_min_keys && p.B * p.H * (p.max_q / QT) <= (int)(CNT_BYTES / 4) - p.B * p.H;
 }
@@ -715,7 +741,7 @@ long attn_q256_workspace_bytes(int B, int H, int max_q, int max_k) {
 int attn_q256_fwd(const AttnParams& p, hipStream_t stream) {
   if (!attn_q256_eligible(p)) return -1;
   const Plan* pl = plan_for(p.B * p.H, p.max_q, p.max_k);
-  if (!pl || pl->ws_bytes > p.split_ws_bytes) return -1;
+  if (!pl || pl->ws_bytes > p.split_ws_bytes || (g_q256_mode == 2 && !pl->wins)) return -1;
   Q256Params q;
   q.a = p;
   q.n_main = p.max_q / QT;

@@ -105,7 +105,7 @@ int flite_attn_varlen_fwd(void* stream, const void* q, const void* k, const void
 
 long flite_attn_workspace_bytes(int batch, int num_heads) { return attn_split_workspace_bytes(batch, num_heads); }
 
-int flite_attn_set_q256(int enable) { return attn_q256_set(enable != 0); }
+int flite_attn_set_q256(int mode) { return attn_q256_set(mode); }
 
 long flite_attn_workspace_bytes_for(int batch, int num_heads, int max_seqlen_q, int max_seqlen_k) {
   if (batch <= 0 || num_heads <= 0 || max_seqlen_q < 0 || max_seqlen_k < 0) return 0;

@@ -108,7 +108,7 @@ long attn_workspace_bytes(int B, int H, int max_q, int max_k);
 // attention_q256.hip: the 256-row route (returns -1 when the launch does not qualify or the workspace is short)
 int attn_q256_fwd(const AttnParams& p, hipStream_t stream);
 long attn_q256_workspace_bytes(int B, int H, int max_q, int max_k);
-int attn_q256_set(int on);  // process-wide route switch (default: FLITE_ATTN_Q256=1 or off)
+int attn_q256_set(int mode);  // process-wide route policy: 0 never, 1 always, 2 by prediction (default)
 
 }  // namespace flite
 

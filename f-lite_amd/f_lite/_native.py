@@ -260,9 +260,10 @@ def attn_workspace(device, batch, num_heads, max_q=0, max_k=0):
     return torch.zeros(n, dtype=torch.uint8, device=device) if n > 0 else None
 
 
-def attn_set_q256(enable: bool):
-    """Route long bounded launches to the 256-query-row kernel (process-wide; include/flite.h flite_attn_set_q256)."""
-    check(load().flite_attn_set_q256(int(bool(enable))), "flite_attn_set_q256")
+def attn_set_q256(mode):
+    """Route policy for long bounded launches (process-wide; include/flite.h flite_attn_set_q256): True / 1 always
+    the 256-query-row kernel, False / 0 never, 2 (the default) where its plan is predicted faster."""
+    check(load().flite_attn_set_q256(int(mode)), "flite_attn_set_q256")
 
 
 def attn_varlen(q, k, v, cu_q, cu_k, max_q, scale, out=None, max_score=0.0, workspace=None, max_k=0):

@@ -19,7 +19,6 @@ import torch  # noqa: E402
 
 from f_lite import _native as nat  # noqa: E402
 
-nat.attn_set_q256(True)
 
 
 def main():
@@ -33,7 +32,10 @@ def main():
     known = {"self": ("self 1024^2", [4112, 4112], [4112, 4112], 12),
              "self1344": ("self 1344x896", [4720, 4720], [4720, 4720], 12),
              "cross": ("cross cond-only", [4112], [512], 12),
-             "round": ("one round 2x4096 H8", [4096, 4096], [4096, 4096], 8)}  # 256 q256 tiles = 1 round, no tail
+             "round": ("one round 2x4096 H8", [4096, 4096], [4096, 4096], 8),
+             "self512": ("self 512^2", [1040, 1040], [1040, 1040], 12),
+             "self1536": ("self 1536^2", [9232, 9232], [9232, 9232], 12),
+             "self7b": ("self 7B 1024^2", [4112, 4112], [4112, 4112], 12)}  # 256 q256 tiles = 1 round, no tail
     shapes = [known[s] for s in args.shapes.split(",")]
     g = torch.Generator(device=dev).manual_seed(3)
 
@@ -53,8 +55,9 @@ def main():
     res = {}
     for r in range(args.rounds):
         for name, a, ws, mk, flops in cases:
-            for kern, kw in (("q128", dict(max_score=16.5, workspace=ws)),
-                             ("q256", dict(max_score=16.5, workspace=ws, max_k=mk))):
+            for kern, mode in (("q128", 0), ("q256", 1), ("auto", 2)):
+                nat.attn_set_q256(mode)
+                kw = dict(max_score=16.5, workspace=ws, max_k=mk)
                 out = nat.attn_varlen(*a, **kw)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

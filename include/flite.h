@@ -89,8 +89,9 @@ long flite_attn_workspace_bytes(int batch, int num_heads);
  * >= flite_attn_workspace_bytes(batch, num_heads).
  */
 long flite_attn_workspace_bytes_for(int batch, int num_heads, int max_seqlen_q, int max_seqlen_k);
-/* Process-wide switch of that 256-query-row route (default off unless FLITE_ATTN_Q256=1 in the environment). */
-int flite_attn_set_q256(int enable);
+/* Process-wide policy of that 256-query-row route: 0 never, 1 always (where eligible), 2 (the default) where its split
+ * plan is predicted >= 4.5 % faster than the 128-row schedule. FLITE_ATTN_Q256=0/1 in the environment sets 0/1. */
+int flite_attn_set_q256(int mode);
 
 /*
  * flite_attn_varlen_fwd with a caller-owned split workspace (device memory, zero-filled once, left zeroed by

@@ -379,9 +379,13 @@ def test_attention_q256(lens_q, lens_k, H):
         new = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
         again = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
     finally:
-        nat.attn_set_q256(False)
+        nat.attn_set_q256(2)
     assert int(ws[:16384].view(torch.int32).abs().sum().item()) == 0  # counters left zeroed
-    old = nat.attn_varlen(*args, max_score=16.5, workspace=ws)  # no max_k: the 128-row kernel
+    nat.attn_set_q256(0)
+    try:
+        old = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))  # the 128-row kernel
+    finally:
+        nat.attn_set_q256(2)
     assert torch.isfinite(new.float()).all()
     ref = torch.empty(q.shape, dtype=torch.float32, device=DEV)  # fp32 reference per (sequence, head), on the GPU
     for b in range(B):
