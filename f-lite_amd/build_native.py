@@ -37,7 +37,10 @@ CFLAGS = [
 # Per-file extra flags. gemm.hip: no SLP vectorisation -- it packs the fp32 epilogue math (RoPE rotation pairs)
 # into v_pk_*_f32 with op_sel shuffles, which needs extra register pairs and spilled 262 VGPRs in the fused qkv
 # epilogue (packed f32 beside MFMAs is an anti-lever anyway: MI355X guide, per-instruction costs).
-FILE_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"], "gemm_fp8.hip": ["-fno-slp-vectorize"]}
+# attention_q256.hip: the same, for the softmax row sums of its two query blocks, which SLP paired into one
+# v_pk_add_f32 chain inside the PV phase (16 per key tile, each ~13 cycles dearer than a v_add_f32 there).
+FILE_FLAGS = {"gemm.hip": ["-fno-slp-vectorize"], "gemm_fp8.hip": ["-fno-slp-vectorize"],
+              "attention_q256.hip": ["-fno-slp-vectorize"]}
 
 
 def _sources():
