@@ -402,11 +402,11 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         const int g = m >> 3, dt = m & 7;
         const s16x8 c = __builtin_shufflevector(lo[m], hi[m], 0, 1, 2, 3, 4, 5, 6, 7);
         const bf16x8 vf = __builtin_bit_cast(bf16x8, c);
+        // P was packed by the previous phase B's softmax, a whole phase A (32 MFMAs) earlier, so no VALU -> MFMA
+        // hazard is left and it is read in place: the NOP form's "+v" operand made hipcc copy each group's P into
+        // a scratch register pair first (2 v_mov_b64 + s_nop per group)
         bf16x8 pk = __builtin_bit_cast(bf16x8, pc[g]);
-        if (dt == 0)
-          mfma_o<true>(o_acc[dt], vf, pk);
-        else
-          mfma_o<false>(o_acc[dt], vf, pk);
+        mfma_o<false>(o_acc[dt], vf, pk);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (EX) softmax_elem(pn, m, e_prev);
         __builtin_amdgcn_sched_barrier(0);
