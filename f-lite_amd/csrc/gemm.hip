@@ -722,6 +722,8 @@ int choose_sk_tiles(const GemmParams& p, int T, int* gs) {
     *gs = 2 * rem;
     return rem;
   }
+  static const bool no_sk = getenv("FLITE_GEMM_NO_SK") != nullptr;  // A/B switch for measurements
+  if (no_sk) return 0;
   return sk::choose_sk_tiles(T, p.K / BK, G, gs);
 }
 
