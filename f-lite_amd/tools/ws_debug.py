@@ -1,6 +1,5 @@
 """Attention on tiny cases against a torch fp32 softmax reference: per-row / per-column error maps (diagnostic; used
 to localise the warp-specialised variant's d-tile corruption, profiles/r05i)."""
-import os
 import sys
 from pathlib import Path
 
@@ -20,7 +19,6 @@ def run(lq, lk, H=1, seed=0):
     cu_k = torch.tensor([0, lk], dtype=torch.int32, device="cuda")
     o = nat.attn_varlen(q, k, v, cu_q, cu_k, lq, D ** -0.5, max_score=16.5, max_k=lk)
     torch.cuda.synchronize()
-    s = (q.float() @ k.float().transpose(0, 1).unsqueeze(0).expand(H, -1, -1).transpose(0, 1).transpose(1, 2)) if False else None
     ref = torch.softmax(torch.einsum("qhd,khd->hqk", q.float(), k.float()) * D ** -0.5, -1)
     ref = torch.einsum("hqk,khd->qhd", ref, v.float())
     return o.float(), ref
