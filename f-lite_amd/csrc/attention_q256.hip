@@ -52,7 +52,10 @@ constexpr int LDS_BYTES = 4 * TILE;  // 64 KiB
 constexpr int SLAB_O_F4 = 4 * 2 * 8 * 4 * 64;
 constexpr int SLAB_FLOATS = SLAB_O_F4 * 4 + 4 * 2 * 64;
 constexpr long SLAB_BYTES = (long)SLAB_FLOATS * 4;
-constexpr long CNT_BYTES = 16384;  // counters at the workspace start: one per split tile, one per tail pair
+// counters at the workspace start: one per split tile, one per tail pair. The same 4 KiB block as the 128-row
+// kernel's (attention.hip CNT_BYTES): a caller's workspace serves both kernels (the engine's attn_ws_), whose slabs
+// overwrite everything past it, and each launch leaves its counters zeroed, so only this block must stay zero.
+constexpr long CNT_BYTES = 4096;
 constexpr int MAX_TAIL = 16;       // key chunks per tail
 constexpr int MIN_KEYS = 1024;     // shorter key ranges keep the 128-row kernel (a tile's prologue dominates)
 

@@ -380,12 +380,20 @@ def test_attention_q256(lens_q, lens_k, H):
         again = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
     finally:
         nat.attn_set_q256(2)
-    assert int(ws[:16384].view(torch.int32).abs().sum().item()) == 0  # counters left zeroed
+    assert int(ws[:4096].view(torch.int32).abs().sum().item()) == 0  # counters left zeroed
     nat.attn_set_q256(0)
     try:
         old = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))  # the 128-row kernel
     finally:
         nat.attn_set_q256(2)
+    # the two kernels share one workspace (the engine's): the 128-row kernel's slabs must not disturb the 256-row
+    # kernel's counters
+    nat.attn_set_q256(True)
+    try:
+        after = nat.attn_varlen(*args, max_score=16.5, workspace=ws, max_k=max(lens_k))
+    finally:
+        nat.attn_set_q256(2)
+    assert torch.equal(new, after)
     assert torch.isfinite(new.float()).all()
     ref = torch.empty(q.shape, dtype=torch.float32, device=DEV)  # fp32 reference per (sequence, head), on the GPU
     for b in range(B):
