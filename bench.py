@@ -347,8 +347,21 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    # FLITE_BENCH_PG=1 at N = 1: run the line through a one-rank RCCL process group anyway, so the multi-GPU code path
+    # (communicator set-up, the timed context broadcast, max over ranks) executes on the one GPU
+    single_pg = world == 1 and os.environ.get("FLITE_BENCH_PG") == "1"
+    if world > 1 or single_pg:
         import torch.distributed as dist
+
+        if single_pg:
+            import socket
+
+            with socket.socket() as so:
+                so.bind(("127.0.0.1", 0))
+                free_port = so.getsockname()[1]
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", str(free_port)), ("RANK", "0"),
+                         ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
 
         if rehearsal:
             dist.init_process_group("gloo")
@@ -580,7 +593,7 @@ def main():
         "distributed": {"world_size": world,
                         "backend": ("gloo REHEARSAL (ranks share %d GPU(s); not a measurement)"
                                     % torch.cuda.device_count() if rehearsal else
-                                    "nccl (RCCL over xGMI)" if world > 1 else "none"),
+                                    "nccl (RCCL over xGMI)" if dist is not None else "none"),
                         "collectives": {
                             "replica": "one broadcast of the [1,512,4096] context from rank 0 before the loop",
                             "cfg-parallel": "context broadcast + per step one all-gather of the two fp32 branch outputs",
