@@ -208,8 +208,9 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
     if (H, W, cfg["per_block_adaln"], cfg["depth"]) == (1024, 1024, True, 40) and steps == 30 and vae is not None:
         # BASELINE.md §4's plan, run once at this workload (`--cpu-baseline-full 2`, 16 cores): the component
         # extrapolation above lands within ~10 % of it
-        out["full_step_check"] = {"per_image_s": 4882, "source": "profiles/r03c/bench_cpu_baseline_full.json: 2 "
-                                  "whole CFG-6 steps 324.6 s + VAE 12.2 s, x15 (10B 1024^2, 16 cores)"}
+        out["full_step_check"] = {"per_image_s": 4389, "source": "profiles/r05j/bench_cpu_baseline_full.log (round "
+                                  "5): 2 whole CFG-6 steps 291.9 s + VAE 11.0 s, x15 (10B 1024^2, 16 cores); round "
+                                  "3: 4882 s (profiles/r03c)"}
     return out
 
 
