@@ -378,6 +378,32 @@ def test_fp8_256_free_running_30_steps(gold3, name, g):
     assert p >= FP8_P3_BARS[(name, g)]
 
 
+@pytest.mark.parametrize("name", ["7b", "10b"])
+def test_fp8_first_blocks_bf16_policy_reaches_40db_at_cfg1(gold3, name):
+    """The quality-leaning MXFP8 policy (DESIGN §5 "fp8 against the reference"): blocks 0-7 keep their bf16 GEMMs, every
+    GEMM class of blocks 8-39 runs MXFP8 (1.40x the bf16 image at 1344x896, profiles/r05m/fp8_block_speed.log). The
+    MXFP8 error enters through the first blocks (bf16 in the LAST four blocks gains 0.1 dB, in the first four 4.9 dB),
+    so this policy meets north_star's 40 dB bar against the reference's fp32 30-step trajectory where CFG noise is
+    absent (CFG 1, 256^2, golden_full3): measured 41.59 / 42.52 dB (7B / 10B) against 35.02 / 35.92 dB all-fp8.
+    At CFG 6 no fp8 policy reaches the reference's own bf16 floor (30.6 dB); that case stays pinned above."""
+    from f_lite import FLitePipeline
+
+    gd, meta = gold3
+    key = f"{name}.256.s30.g1"
+    m = DiT.random(seed=0, device=DEV, **PRESETS[name])
+    m.enable_fp8(True, bf16_blocks=list(range(8)))
+    ctx = torch.empty(*meta["inputs"]["ctx"][1], device=DEV, dtype=torch.bfloat16)
+    nat.init_param_(ctx, meta["inputs"]["ctx"][0], seed=0, std=1.0)
+    lat = torch.empty(*meta["inputs"]["latents_256"][1], device=DEV, dtype=torch.bfloat16)
+    nat.init_param_(lat, meta["inputs"]["latents_256"][0], seed=0, std=1.0)
+    out = FLitePipeline(m)(prompt_embeds=ctx, latents=lat, height=256, width=256, num_inference_steps=30,
+                           guidance_scale=1.0, output_type="latent").images.float().cpu()
+    p = psnr(out / 0.3611 + 0.1159, gd[f"{key}.f32.final"])
+    print(f"fp8 (bf16 blocks 0-7) {name} 256^2 30-step CFG-1 final latents: {p:.2f} dB vs reference fp32 "
+          f"(reference's own bf16 run: {meta[f'{key}.bf16_vs_f32_psnr']:.2f} dB)")
+    assert p >= 40.0
+
+
 def test_fp8_10b_1344x896_30_steps_full_loop():
     """BASELINE configs[4] at full size: the 10B MXFP8 loop at 1344x896, 30 CFG-6 steps, tiled VAE
     decode to uint8, as bench.py --fp8 runs it: hipGraph == eager bit for bit, finite, and the uint8 image within a

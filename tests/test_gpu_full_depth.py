@@ -320,3 +320,30 @@ def test_10b_1024_30_steps_vs_reference(gold4, m7b, m10b, name, g):
     else:
         assert ifloor is not None, f"{key}.image_bf16_vs_f32_psnr missing: the bf16 trajectory's image"
         assert pi >= ifloor
+
+
+@pytest.mark.parametrize("name", ["10b", "7b"])
+def test_fp8_first_blocks_bf16_1024_cfg1_vs_reference(gold4, m7b, m10b, name):
+    """BASELINE configs[4]'s MXFP8 path at the metric's size against the reference itself (DESIGN §5 "fp8 against the
+    reference"): 1024^2, 30 steps, CFG 1 (no CFG amplification), final latents vs the reference's fp32 trajectory.
+    The quality-leaning policy (blocks 0-7 bf16, every GEMM class MXFP8 in blocks 8-39; 1.40x the bf16 image) must
+    meet the SURVEY §8d bar of 40 dB. The all-fp8 policy is printed beside it; it is the BASELINE row and the default,
+    and no bar applies to it here."""
+    gd, meta = gold4
+    key = f"{name}.1024.s30.g1"
+    if f"{key}.f32.final" not in gd:
+        pytest.skip(f"{key} not in the fixture file")
+    model = m7b if name == "7b" else m10b
+    kw = dict(prompt_embeds=hashed(meta, "ctx"), latents=hashed(meta, "latents_1024"), height=1024, width=1024,
+              num_inference_steps=30, guidance_scale=1.0, output_type="latent")
+    res = {}
+    try:
+        for label, blocks in (("all fp8", []), ("bf16 blocks 0-7", list(range(8)))):
+            model.enable_fp8(True, bf16_blocks=blocks)
+            lat = FLitePipeline(model)(**kw).images.float()
+            res[label] = psnr(lat / SCALING + SHIFT, gd[f"{key}.f32.final"])
+    finally:
+        model.enable_fp8(False, bf16_blocks=[])
+    print(f"fp8 {name} 1024^2 30-step CFG-1 final latents vs reference fp32: " +
+          ", ".join(f"{k} {v:.2f} dB" for k, v in res.items()))
+    assert res["bf16 blocks 0-7"] >= 40.0
