@@ -654,7 +654,9 @@ Plan make_plan(int cus, int pairs, int max_q, int max_k) {
   static const int kTails[] = {1, 2, 3, 4, 6, 8, 10, 12, 16};
   for (int ti = 0; ti < (tail_rows > 0 ? 9 : 1); ++ti) {
     const int nt = tail_rows > 0 ? kTails[ti] : 0;
-    for (int s = 0; s <= F; ++s) {
+    // halving more than two rounds' worth of tiles only lengthens the list (a half costs 0.6 of a whole tile), so
+    // the search stops there: O(CUs * F) simulations instead of O(F^2) for large batches
+    for (int s = 0; s <= std::min(F, 2 * cus); ++s) {
       const double m = simulate(cus, F - s, s, pairs, nt, nk, tail_rows);
       if (m < best - 1e-9) {
         best = m;
@@ -736,6 +738,8 @@ bool attn_q256_eligible(const AttnParams& p) {
 
 long attn_q256_workspace_bytes(int B, int H, int max_q, int max_k) {
   if (q256_init() || max_q < QT || max_k < g_min_keys) return 0;
+  // launches past the counter block never take this route (attn_q256_eligible): no plan, no slabs
+  if ((long)B * H * (max_q / QT) > (long)(CNT_BYTES / 4) - (long)B * H) return 0;
   const Plan* pl = plan_for(B * H, max_q, max_k);
   return pl ? pl->ws_bytes : 0;
 }
