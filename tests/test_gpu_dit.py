@@ -138,6 +138,29 @@ def test_sampling_loop_vs_oracle(golden, tiny, tiny_ref, key, g, apg):
     assert p >= 35.0
 
 
+def test_num_images_per_prompt_repeats_each_prompt(tiny, tiny_ref):
+    """num_images_per_prompt (reference pipeline.py: prompt and negative embeddings repeat_interleave'd, one latent per
+    image): two prompts x 2 images run the same launches as the prompts passed p0, p0, p1, p1 explicitly, bit for
+    bit, and the batched CFG-6 loop matches the fp32 oracle's batched loop on those repeated embeddings."""
+    g = torch.Generator().manual_seed(11)
+    L, C = 24, tiny.config.cross_attn_input_size
+    pos = torch.randn(2, L, C, generator=g).bfloat16()
+    neg = torch.randn(2, L, C, generator=g).bfloat16()
+    lat = torch.randn(4, 16, 16, 16, generator=g).bfloat16()
+    pipe = FLitePipeline(tiny)
+    kw = dict(height=128, width=128, num_inference_steps=4, guidance_scale=6.0, output_type="latent")
+    a = pipe(prompt_embeds=pos.to(DEV), negative_prompt_embeds=neg.to(DEV), num_images_per_prompt=2,
+             latents=lat.to(DEV), **kw).images.float().cpu()
+    pos2, neg2 = pos.repeat_interleave(2, dim=0), neg.repeat_interleave(2, dim=0)
+    b = pipe(prompt_embeds=pos2.to(DEV), negative_prompt_embeds=neg2.to(DEV), latents=lat.to(DEV), **kw).images
+    assert a.shape == (4, 16, 16, 16) and torch.equal(a, b.float().cpu())
+    ref = R.sample(tiny_ref, lat.float(), pos2.float(), neg2.float(), num_steps=4, guidance_scale=6.0,
+                   apg=R.APG(enabled=False), height=128, width=128, t_dtype=torch.bfloat16, acc_dtype=torch.float32)
+    p = psnr(a, ref)
+    print(f"num_images_per_prompt=2, 2 prompts, CFG 6: PSNR vs fp32 oracle {p:.2f} dB")
+    assert p >= 35.0
+
+
 def test_graph_replay_equals_eager(golden, tiny):
     a = _pipe_latents(tiny, golden, 6.0, use_graph=False)
     b = _pipe_latents(tiny, golden, 6.0, use_graph=True)
