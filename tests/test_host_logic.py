@@ -69,6 +69,22 @@ def test_schedule_matches_reference(golden_meta):
         assert [(t, dt) for t, dt in got] == [tuple(r) for r in rows]
 
 
+def test_schedule_explicit_alpha():
+    """__call__'s alpha (reference pipeline.py:239-256): an explicit alpha replaces 2*sqrt(tokens / 64^2); alpha = 1
+    is the unshifted linear schedule t = i/n, dt = 1/n; the shifted t stay in (0, 1], decrease, and the dt sum to 1."""
+    lin = flow_schedule(8, 128, 128, alpha=1.0)
+    assert [t for t, _ in lin] == [i / 8 for i in range(8, 0, -1)]
+    assert all(abs(dt - 1 / 8) < 1e-15 for _, dt in lin)
+    for a in (0.5, 3.0, 7.5):
+        s = flow_schedule(30, 96, 160, alpha=a)
+        ts = [t for t, _ in s]
+        assert ts[0] == 1.0 and all(0.0 < x <= 1.0 for x in ts) and all(x > y for x, y in zip(ts, ts[1:]))
+        assert abs(sum(dt for _, dt in s) - 1.0) < 1e-12
+        i = 10  # the 21st step: t = i/n shifted by alpha
+        assert s[30 - i][0] == (i / 30) * a / (1 + (a - 1) * (i / 30))
+    assert flow_schedule(30, 128, 128) == flow_schedule(30, 128, 128, alpha=2 * (128 * 128 / 64 ** 2) ** 0.5)
+
+
 def test_forward_on_cpu_raises():
     m = DiT(**PRESETS["tiny"])
     with pytest.raises(FliteError):
