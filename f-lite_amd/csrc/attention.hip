@@ -755,7 +755,17 @@ int attn_fwd(const AttnParams& p, hipStream_t stream) {
       pairs <= (int)(CNT_BYTES / 4) &&
       (p.max_k <= 0 || p.max_k >= MIN_SPLIT_KEYS)) {
     const long cap = (p.split_ws_bytes - CNT_BYTES) / SLAB_BYTES / pairs;  // slabs per pair in the workspace
-    const int S = (int)std::min<long>(std::min(g_attn_cus / pairs, MAX_SPLIT), cap);
+    int S = (int)std::min<long>(std::min(g_attn_cus / pairs, MAX_SPLIT), cap);
+    // only live chunks (512 keys = 8 tiles over 16 chunks: 8 of them empty): with per = ceil(tiles / S) tiles per
+    // chunk, ceil(tiles / per) chunks cover the keys with the same per (checked for every tiles < 600, S <= 16), so
+    // the longest sequences keep their partition and slab-order sum (shorter ones of a ragged launch may be cut
+    // differently, still deterministically); an empty chunk only added a prologue, a zero slab and a hand-off at the
+    // head of the launch (split_first)
+    if (p.max_k > 0 && S >= 2) {
+      const int n_kt = (p.max_k + KT - 1) / KT;
+      const int per = (n_kt + S - 1) / S;
+      S = (n_kt + per - 1) / per;
+    }
     if (S >= 2) {
       q.n_main = p.max_q / QT;
       q.n_split = S;
