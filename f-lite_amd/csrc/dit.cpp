@@ -563,8 +563,14 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   const int Bsa = sa_seqs_ > 0 ? sa_seqs_ : B_;
   const long Msa = (long)Bsa * Tl_;
   auto norm = [&](const bf16_t* w, const float* sh, const float* sc, const bf16_t* pf0 = nullptr, long pf0_n = 0,
-                  const bf16_t* pf1 = nullptr, long pf1_n = 0, long rows = 0) -> int {
+                  const bf16_t* pf1 = nullptr, long pf1_n = 0, long rows = 0, const float* bc_c = nullptr,
+                  const float* bc_gate = nullptr, long bc_rows = 0) -> int {
     NormModParams nm;
+    nm.bc_c = bc_c;
+    nm.bc_gate = bc_gate;
+    nm.bc_gate_stride = mseg;
+    nm.bc_rows = bc_rows;
+    nm.bc_rows_per_seg = Tl_;
     if (norm_prefetch()) {
       nm.pf[0] = pf0;
       nm.pf_bytes[0] = pf0_n * 2;
@@ -679,9 +685,14 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   // --- cross attention (model.py:291-297) ---
   // The first ctx_uni_ sequences have uniform context (set_context): their rows take the step-invariant
   // x += gate_ca * c; the norm, the cross-q GEMM, the attention and the cross-proj run on the other rows only.
+  // Nothing reads the collapsed rows of x before norm3, so their update x += gate_ca * c is deferred into norm3's
+  // read of those rows (one 50 MB fp32 read-modify-write pass fewer per block; the same fma, bit for bit).
+  // (the D = 3072 row kernel takes the update; other widths keep the separate pass here)
   const int U = b.cross ? ctx_uni_ : 0;
   const long r0 = (long)U * Tl_;
-  if (U > 0 && ctx_bcast_resid(x_, ctx_c_ + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s)) return 1;
+  const bool bc_defer = U > 0 && D == 3072;
+  const float* bc_c = bc_defer ? ctx_c_ + (long)blk * B_ * D : nullptr;
+  if (U > 0 && !bc_defer && ctx_bcast_resid(x_, ctx_c_ + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s)) return 1;
   if (b.cross && r0 < M_) {
     {
       NormModParams nm;
@@ -768,7 +779,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   }
 
   // --- SwiGLU MLP (model.py:299-301) ---
-  if (norm(b.norm3, shift_mlp, scale_mlp)) return 1;
+  if (norm(b.norm3, shift_mlp, scale_mlp, nullptr, 0, nullptr, 0, 0, bc_c, gate_ca, bc_defer ? r0 : 0)) return 1;
   {
     GemmParams g;
     g.A = nbuf_;

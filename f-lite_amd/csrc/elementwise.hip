@@ -106,7 +106,8 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(NormModParams p) {
 // a wave reduction plus 4 partials through LDS.
 // PF: the weight read-ahead below is compiled in; the PF = false instantiation is the plain kernel (the
 // read-ahead's registers and loads had cost every launch ~8 us, round-2 VERDICT item 4).
-template <bool IN_BF16, int NQ, bool OUT8 = false, bool PF = false>
+// BC: the deferred broadcast residual of NormModParams (bc_*), applied to the fp32 row before the reduction.
+template <bool IN_BF16, int NQ, bool OUT8 = false, bool PF = false, bool BC = false>
 __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
   __shared__ float part[4];
   const int t = threadIdx.x;
@@ -133,6 +134,21 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
       v[4 * q + 1] = w[1];
       v[4 * q + 2] = w[2];
       v[4 * q + 3] = w[3];
+    }
+    if constexpr (BC) {
+      if (m < p.bc_rows) {  // uniform over the workgroup (one row)
+        const long bs = m / p.bc_rows_per_seg;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int n = q * 1024 + t * 4;
+          const f32x4 cv = *(const f32x4*)(p.bc_c + bs * (long)(1024 * NQ) + n);
+          const f32x4 gv = *(const f32x4*)(p.bc_gate + bs * p.bc_gate_stride + n);
+          f32x4 nv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) nv[j] = v[4 * q + j] = __builtin_fmaf(cv[j], gv[j], v[4 * q + j]);
+          *(f32x4*)((float*)p.x + in_row * p.ldx + n) = nv;  // ctx_bcast_resid_kernel's fma, in place
+        }
+      }
     }
   }
   // weight, scale and shift (L2-resident, shared by all rows) are loaded before the reduction, so the row's
@@ -618,6 +634,8 @@ int grid_for(long total, int per_block = 256) {
 
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   FLITE_REQUIRE(p.ldx % 4 == 0 && p.ldy % 4 == 0, "rmsnorm: strides must be multiples of 4");
+  FLITE_REQUIRE(p.bc_rows <= 0 || (p.D == 3072 && p.y8 == nullptr && p.rows < (1L << 31)),
+                "rmsnorm: the deferred broadcast residual is implemented for the D = 3072 bf16-output row kernel only");
   if (p.rows <= 0) return 0;
   if (p.y8 != nullptr) {  // MXFP8 output (fp8 DiT path): fp32 input rows only
     FLITE_REQUIRE(!in_bf16 && p.ysc != nullptr && p.ysc_rows_pad >= mx_rows_pad(p.rows) && p.D % 128 == 0 &&
@@ -639,7 +657,13 @@ int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   }
   if (p.D == 3072 && p.rows < (1L << 31)) {  // the DiT width: one workgroup per row
     const bool pf = p.pf[0] != nullptr || p.pf[1] != nullptr;
-    if (in_bf16)
+    if (p.bc_rows > 0) {
+      FLITE_REQUIRE(!in_bf16 && !pf && p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate &&
+                        p.bc_rows_per_seg > 0,
+                    "rmsnorm: the deferred broadcast residual needs fp32 rows in place, no read-ahead");
+      hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, false, false, true>), dim3((unsigned)p.rows), dim3(256), 0,
+                         s, p);
+    } else if (in_bf16)
       hipLaunchKernelGGL((rmsnorm_mod_row_kernel<true, 3>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
     else if (pf)
       hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, false, true>), dim3((unsigned)p.rows), dim3(256), 0, s,

@@ -138,6 +138,14 @@ struct NormModParams {
   // once by the workgroups of this pass so that they come from the Infinity Cache instead of HBM
   const void* pf[2] = {nullptr, nullptr};
   long pf_bytes[2] = {0, 0};
+  // optional deferred broadcast residual (D = 3072 row kernel, fp32 input, identity row mapping): rows m < bc_rows
+  // first take x[m] += bc_gate[seg] * bc_c[seg], seg = m / bc_rows_per_seg, written back to x (the collapsed
+  // sequences' cross-attention update, ctx_bcast_resid's expression), then normalise
+  const float* bc_c = nullptr;
+  const float* bc_gate = nullptr;
+  long bc_gate_stride = 0;
+  long bc_rows = 0;
+  int bc_rows_per_seg = 1;
 };
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s);
 
