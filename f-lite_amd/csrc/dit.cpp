@@ -955,7 +955,8 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   const int Bsa = sa_seqs_ > 0 ? sa_seqs_ : B_;  // as run_block: block 0 of a CFG batch, self-attention once
   const long Msa = (long)Bsa * Tl_;
   const bool probe_sa = Msa == M_;
-  auto norm8 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0, long r0 = 0) -> int {
+  auto norm8 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0, long r0 = 0,
+                    const float* bc_c = nullptr, long bc_rows = 0) -> int {
     NormModParams nm;  // rows [r0, r0 + rows) of x; r0 % 4 == 0 keeps the scale rows 16-B aligned (uni_fp8)
     nm.x = x_ + r0 * D;
     nm.ldx = D;
@@ -972,6 +973,11 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     nm.in_seg = Tl_;
     nm.in_stride = Tl_;
     nm.in_off = 0;
+    nm.bc_c = bc_c;  // the collapsed rows' deferred update (norm3 only; run_block's note)
+    nm.bc_gate = gate_ca;
+    nm.bc_gate_stride = mseg;
+    nm.bc_rows = bc_rows;
+    nm.bc_rows_per_seg = Tl_;
     return rmsnorm_mod(nm, false, s);
   };
   auto g8 = [&](const uint8_t* A, const uint8_t* As, const uint8_t* W, const uint8_t* Ws, long w_rows, int N, int K,
@@ -1057,7 +1063,8 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   const int cm = fp8_classes_;
   const bool f_qkv = cm & FLITE_FP8_QKV, f_proj = cm & FLITE_FP8_PROJ, f_cq = cm & FLITE_FP8_CROSS_Q,
              f_cproj = cm & FLITE_FP8_CROSS_PROJ, f_gu = cm & FLITE_FP8_GATE_UP, f_down = cm & FLITE_FP8_DOWN;
-  auto norm16 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0, long r0 = 0) -> int {
+  auto norm16 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0, long r0 = 0,
+                    const float* bc_c = nullptr, long bc_rows = 0) -> int {
     NormModParams nm;
     nm.x = x_ + r0 * D;
     nm.ldx = D;
@@ -1072,6 +1079,11 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     nm.in_seg = Tl_;
     nm.in_stride = Tl_;
     nm.in_off = 0;
+    nm.bc_c = bc_c;
+    nm.bc_gate = gate_ca;
+    nm.bc_gate_stride = mseg;
+    nm.bc_rows = bc_rows;
+    nm.bc_rows_per_seg = Tl_;
     return rmsnorm_mod(nm, false, s);
   };
   auto g16 = [&](const bf16_t* A, const bf16_t* W, int N, const bf16_t* bias, int epi, void* out, long ldo,
@@ -1127,7 +1139,11 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   const bool f_ca = f_cq || f_cproj;
   const int U = b.cross ? (f_ca ? uni_fp8() : ctx_uni_) : 0;
   const long r0 = (long)U * Tl_, rows = M_ - r0;
-  if (U > 0 && ctx_bcast_resid(x_, (f_cproj ? ctx_c8_ : ctx_c_) + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s))
+  // deferred into norm3's read of the collapsed rows at D = 3072, as in run_block
+  const bool bc_defer = U > 0 && D == 3072;
+  const float* bc_c = bc_defer ? (f_cproj ? ctx_c8_ : ctx_c_) + (long)blk * B_ * D : nullptr;
+  if (U > 0 && !bc_defer &&
+      ctx_bcast_resid(x_, (f_cproj ? ctx_c8_ : ctx_c_) + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s))
     return 1;
   if (b.cross && rows > 0) {
     if (f_cq ? norm8(b.norm2, shift_ca + U * mseg, scale_ca + U * mseg, rows, r0)
@@ -1158,7 +1174,9 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   }
   // --- SwiGLU MLP --- (an fp8 gate/up writes the SwiGLU output as MXFP8 for an fp8 down, bf16 for a bf16 down; a
   // bf16 gate/up feeding an fp8 down is quantised by quant_rows_fp8)
-  if (f_gu ? norm8(b.norm3, shift_mlp, scale_mlp) : norm16(b.norm3, shift_mlp, scale_mlp)) return 1;
+  if (f_gu ? norm8(b.norm3, shift_mlp, scale_mlp, 0, 0, bc_c, bc_defer ? r0 : 0)
+           : norm16(b.norm3, shift_mlp, scale_mlp, 0, 0, bc_c, bc_defer ? r0 : 0))
+    return 1;
   if (probe_begin(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
   if (f_gu) {
     if (f_down ? g8(nbuf8_, nbuf8_s_, q.gu, q.gu_s, 2L * F, 2 * F, D, nullptr, EPI8_SWIGLU_FP8, hbuf8_, F, nullptr)

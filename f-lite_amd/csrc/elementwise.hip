@@ -634,15 +634,22 @@ int grid_for(long total, int per_block = 256) {
 
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   FLITE_REQUIRE(p.ldx % 4 == 0 && p.ldy % 4 == 0, "rmsnorm: strides must be multiples of 4");
-  FLITE_REQUIRE(p.bc_rows <= 0 || (p.D == 3072 && p.y8 == nullptr && p.rows < (1L << 31)),
-                "rmsnorm: the deferred broadcast residual is implemented for the D = 3072 bf16-output row kernel only");
+  FLITE_REQUIRE(p.bc_rows <= 0 || (p.D == 3072 && p.rows < (1L << 31)),
+                "rmsnorm: the deferred broadcast residual is implemented for the D = 3072 row kernel only");
   if (p.rows <= 0) return 0;
   if (p.y8 != nullptr) {  // MXFP8 output (fp8 DiT path): fp32 input rows only
     FLITE_REQUIRE(!in_bf16 && p.ysc != nullptr && p.ysc_rows_pad >= mx_rows_pad(p.rows) && p.D % 128 == 0 &&
                       p.ldy % 16 == 0,
                   "rmsnorm(fp8 out): fp32 input, scales for the padded rows, D % 128, 16-B row stride");
     if (p.D == 3072) {
-      hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, true>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
+      if (p.bc_rows > 0) {
+        FLITE_REQUIRE(p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
+                      "rmsnorm(fp8 out): the deferred broadcast residual needs fp32 rows in place");
+        hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, true, false, true>), dim3((unsigned)p.rows), dim3(256), 0,
+                           s, p);
+      } else {
+        hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, true>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
+      }
     } else {
       const int grid8 = (int)((p.rows + 3) / 4);
       switch (p.D / 256) {

@@ -19,6 +19,8 @@ from f_lite import DiT, FLitePipeline
 from f_lite.model import PRESETS
 cfg = dict(PRESETS[{preset!r}], depth={depth})
 m = DiT.random(seed=0, device="cuda", **cfg)
+if {fp8}:
+    m.enable_fp8(True)
 g = torch.Generator().manual_seed(6)
 hw = {size}
 lat = torch.randn(2, 16, hw // 8, hw // 8, generator=g).bfloat16().cuda()
@@ -37,12 +39,14 @@ def main():
     ap.add_argument("--preset", default="10b")
     ap.add_argument("--depth", type=int, default=2)
     ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--fp8", action="store_true", help="the MXFP8 blocks (DiT.enable_fp8)")
     a = ap.parse_args()
     import torch
 
     key, val = a.var.split("=", 1)
     script = Path("/tmp/env_equal_child.py")
-    script.write_text(CHILD.format(pkg=str(ROOT / "f-lite_amd"), preset=a.preset, depth=a.depth, size=a.size))
+    script.write_text(CHILD.format(pkg=str(ROOT / "f-lite_amd"), preset=a.preset, depth=a.depth, size=a.size,
+                                        fp8=bool(a.fp8)))
     outs = []
     for i, extra in enumerate(({}, {key: val})):
         env = dict(os.environ)
