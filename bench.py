@@ -125,16 +125,16 @@ def cpu_threads() -> "tuple[int, str]":
     return max(1, n), f"no cgroup CPU quota ({info['cgroup_cpu_max']}); all {n} affinity cores"
 
 
-def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blocks: int = 3):
+def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blocks: int = 3, vae_s=None):
     """The fp32 CPU port of the path (oracle/flite_ref.py + oracle/vae_ref.py, checked against the stub-loaded
     reference's golden fixtures) timed on this node's host cores, on the same bf16 weights copied to the host.
 
-    A full CPU image is ~1.5 h at 10B 1024^2, so the sample measures every DIFFERENT piece of one image once and
-    extrapolates: (a) the per-call DiT work outside the blocks (context_proj + norm, patch embed, time embed /
-    adaLN, final stage; RefDiT at depth 0) at the CFG batch of 2, (b) `n_blocks` DiT blocks at full size (every
-    block of a layout has the same shapes), (c) one full VAE decode to uint8 when a VAE is present. Per image =
-    steps x (a + depth x b / n_blocks) + c, labelled as extrapolated. (BASELINE.md §4 plans 2 whole CFG steps
-    + VAE x15; on a 16-core share that is ~6 min of CPU, beyond the bounded sample the bench contract allows.)"""
+    The component sample (the cross-check of cpu_baseline_full's whole step since round 6; `--cpu-baseline-full 0`
+    makes it the value): measures every DIFFERENT piece of one image once and extrapolates: (a) the per-call DiT
+    work outside the blocks (context_proj + norm, patch embed, time embed / adaLN, final stage; RefDiT at depth 0)
+    at the CFG batch of 2, (b) `n_blocks` DiT blocks at full size (every block of a layout has the same shapes),
+    (c) one full VAE decode to uint8 when a VAE is present (or `vae_s`, a decode already timed). Per image =
+    steps x (a + depth x b / n_blocks) + c, labelled as extrapolated."""
     import dataclasses
 
     from oracle import flite_ref as R
@@ -180,8 +180,8 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
             x = ref.block(i, x, cu, T, ctx, ccu, mod, cos, sin)
         res["block_s"] = (time.perf_counter() - t0) / n_blocks
         # (c) one VAE decode to uint8
-        res["vae_s"] = 0.0
-        if vae is not None:
+        res["vae_s"] = 0.0 if vae_s is None else float(vae_s)
+        if vae is not None and vae_s is None:
             vparams = {n: t.detach().float().cpu() for n, t in vae.named_parameters()}
             dec = VR.RefVAEDecoder(vparams)
             z = torch.randn(1, 16, H // 8, W // 8, generator=g)
@@ -205,20 +205,14 @@ def cpu_baseline_sample(model, vae, cfg: dict, H: int, W: int, steps: int, n_blo
         "host": host_info(),
         "components_s": {k: round(v, 3) for k, v in res.items()},
     }
-    if (H, W, cfg["per_block_adaln"], cfg["depth"]) == (1024, 1024, True, 40) and steps == 30 and vae is not None:
-        # BASELINE.md §4's plan, run once at this workload (`--cpu-baseline-full 2`, 16 cores): the component
-        # extrapolation above lands within ~10 % of it
-        out["full_step_check"] = {"per_image_s": 4389, "source": "profiles/r05j/bench_cpu_baseline_full.log (round "
-                                  "5): 2 whole CFG-6 steps 291.9 s + VAE 11.0 s, x15 (10B 1024^2, 16 cores); round "
-                                  "3: 4882 s (profiles/r03c)"}
     return out
 
 
-def cpu_baseline_full(model, vae, cfg: dict, H: int, W: int, steps: int, k_steps: int = 2):
-    """BASELINE.md §4's plan: K whole CFG-batched denoise steps of the fp32 CPU port (every block, the CFG
-    combine and Euler update) + one VAE decode, per image = (steps / K) x the K steps + the decode, labelled
-    extrapolated. Minutes of CPU at 10B 1024^2: a one-off measurement (`--cpu-baseline-full K`), not part of
-    the default bounded bench."""
+def cpu_baseline_full(model, vae, cfg: dict, H: int, W: int, steps: int, k_steps: int = 1):
+    """BASELINE.md §4's plan and the default `cpu_baseline` since round 6: K whole CFG-batched denoise steps of the
+    fp32 CPU port (every block, the CFG combine and Euler update) + one VAE decode, per image = (steps / K) x the K
+    steps + the decode, labelled extrapolated. K = 1 at 10B 1024^2 is ~2.5 min of CPU on the box's 16-core
+    share: one measured step of the 30, each of which does the same work (the schedule changes only t)."""
     from oracle import flite_ref as R
     from oracle import vae_ref as VR
 
@@ -299,9 +293,10 @@ def main():
     ap.add_argument("--vae-tiling", action="store_true",
                     help="pipe.enable_vae_tiling() as generate.py:77-78 does (tiled decode above 1024 px)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-baseline-full", type=int, default=0, metavar="K",
-                    help="CPU baseline from K whole CFG steps + VAE (BASELINE.md §4; minutes of CPU) instead of the "
-                         "bounded per-component sample")
+    ap.add_argument("--cpu-baseline-full", type=int, default=1, metavar="K",
+                    help="CPU baseline from K whole CFG steps + VAE, x steps/K (BASELINE.md §4; ~2.5 min of CPU per "
+                         "step at 10B 1024^2 on 16 cores), with the per-component sample beside it as a cross-check; "
+                         "0: the per-component sample alone")
     ap.add_argument("--images-per-gpu", type=int, default=1,
                     help="images per bench step and GPU, sampled as ONE batch (num_images_per_prompt; M = 2 x B x T)")
     ap.add_argument("--fp8", action="store_true",
@@ -554,8 +549,14 @@ def main():
     cpu = None
     if not args.no_cpu_baseline and world == 1:  # at N = 1 only (rank 0)
         if args.cpu_baseline_full > 0:
+            # the value: whole measured CFG step(s) + VAE; the component sample beside it as the cross-check
             cpu = cpu_baseline_full(model, vae, cfg, args.height, args.width, args.sample_steps,
                                     args.cpu_baseline_full)
+            chk = cpu_baseline_sample(model, vae, cfg, args.height, args.width, args.sample_steps, n_blocks=1,
+                                      vae_s=cpu["components_s"]["vae_s"])
+            cpu["components_check"] = {"per_image_s": round(1.0 / chk["value"], 1), "sample": chk["sample"],
+                                       "components_s": chk["components_s"],
+                                       "ratio_to_value": round(cpu["value"] / chk["value"], 4)}
         else:
             cpu = cpu_baseline_sample(model, vae, cfg, args.height, args.width, args.sample_steps)
 

@@ -152,6 +152,26 @@ def test_cpu_baseline_threads_follow_cgroup_quota(monkeypatch):
     assert set(q) == {"cgroup_cpu_max", "cgroup_cpus"}
 
 
+def test_cpu_baseline_whole_step_with_component_check():
+    """bench.cpu_baseline_full (the default `cpu_baseline` since round 6): whole measured CFG
+    step(s) of the fp32 port extrapolated x steps/K, and the per-component sample beside it (shape of the record on
+    a tiny model; the GPU box runs the 10B 1024^2 workload)."""
+    import bench
+    from oracle.weights import make_param, param_shapes
+
+    cfg = dict(PRESETS["tiny"])
+
+    class _Params:
+        def named_parameters(self):
+            return [(k, make_param(k, v)) for k, v in param_shapes(cfg).items()]
+
+    full = bench.cpu_baseline_full(_Params(), None, cfg, 64, 64, 4, k_steps=1)
+    assert full["kind"] == "port" and full["extrapolated"] and full["value"] > 0
+    assert "1 whole CFG-6 steps of the 4-step schedule" in full["sample"]
+    chk = bench.cpu_baseline_sample(_Params(), None, cfg, 64, 64, 4, n_blocks=1, vae_s=full["components_s"]["vae_s"])
+    assert chk["value"] > 0 and chk["components_s"]["vae_s"] == 0.0
+
+
 class _PointwiseDecoder:
     """Stand-in decoder whose pixel (y, x) depends only on latent (y // 8, x // 8): any correct tiling of it
     (grid, in-place blends of equal overlaps, crops, concatenation) reproduces the untiled output exactly."""
