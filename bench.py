@@ -310,6 +310,12 @@ def main():
     ap.add_argument("--fp8-classes", default="all",
                     help="with --fp8: GEMM classes on MXFP8 (comma-separated _native.FP8_CLASSES names: qkv, proj, "
                          "cross_q, cross_proj, gate_up, down; 'all'), the others bf16 (precision policy)")
+    ap.add_argument("--fp8-block-classes", default="",
+                    help="with --fp8: per-block class policy, _native.fp8_block_masks syntax (e.g. "
+                         "'0-3:none;4-7:gate_up+qkv'); overrides --fp8-classes for the blocks it names")
+    ap.add_argument("--residual", default=None, choices=["fp32", "bf16"],
+                    help="residual-stream storage (DiT.set_residual_dtype); default: the engine's (fp32 unless "
+                         "FLITE_RESID_BF16=1)")
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
     ap.add_argument("--mode", default="replica", choices=["replica", "cfg-parallel", "sp", "sp-ring"],
                     help="replica: image i on GPU i mod N (the metric line); cfg-parallel: the two CFG branches of an "
@@ -374,9 +380,14 @@ def main():
 
     cfg = dict(PRESETS[args.model])
     model = DiT.random(seed=0, device=dev, **cfg)
+    if args.residual is not None:
+        model.set_residual_dtype(torch.bfloat16 if args.residual == "bf16" else torch.float32)
     keep16 = [int(b) for b in args.fp8_bf16_blocks.split(",") if b.strip()]
+    fp8_mask = nat.fp8_class_mask(args.fp8_classes) if args.fp8 else None
+    blk_masks = (nat.fp8_block_masks(args.fp8_block_classes, cfg["depth"], fp8_mask)
+                 if args.fp8 and args.fp8_block_classes else None)
     if args.fp8:
-        model.enable_fp8(True, bf16_blocks=keep16, gemm_classes=args.fp8_classes)
+        model.enable_fp8(True, bf16_blocks=keep16, gemm_classes=fp8_mask, block_classes=blk_masks)
     vae = None
     if not args.no_vae:
         from f_lite.vae import AutoencoderKL
@@ -591,7 +602,10 @@ def main():
                                    "sp-ring": "sequence parallel sp%d (ring K/V shifts)" % world}[args.mode],
                    "hipgraph": not args.no_graph, "vae_tiling": bool(args.vae_tiling),
                    "fp8_bf16_blocks": keep16 if args.fp8 else None,
-                   "fp8_classes": args.fp8_classes if args.fp8 else None},
+                   "fp8_classes": args.fp8_classes if args.fp8 else None,
+                   "fp8_class_mask": fp8_mask,
+                   "fp8_block_classes": (args.fp8_block_classes or None) if args.fp8 else None,
+                   "residual_dtype": "bf16" if model.engine().residual_bf16() else "fp32"},
         "distributed": {"world_size": world,
                         "backend": ("gloo REHEARSAL (ranks share %d GPU(s); not a measurement)"
                                     % torch.cuda.device_count() if rehearsal else

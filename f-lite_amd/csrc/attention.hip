@@ -319,6 +319,7 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
     };
     constexpr int KAHEAD = 3;  // K fragment reads issued this many k-steps ahead of their MFMA pair
     constexpr int VAHEAD = 4;  // V^T transposed reads issued this many MFMAs ahead
+    static_assert(VAHEAD >= 1, "attn_common.h mfma_o: the read-ahead block separates the softmax from the PV MFMAs");
     f32x16 s0, s1;          // S of the tile whose softmax is pending
     u32x4 pa[4], pb[4];     // P^T operands (kh, 16-key half) of two consecutive tiles, bf16 pairs
     // phase A. KB: K buffer read by the S MFMAs; DKB / DVB: buffers the K / V copies land in; DMA: copies issued
@@ -402,9 +403,9 @@ __global__ __launch_bounds__(NT, 1) void attn_fwd_hd256_kernel(AttnParams p) {
         const int g = m >> 3, dt = m & 7;
         const s16x8 c = __builtin_shufflevector(lo[m], hi[m], 0, 1, 2, 3, 4, 5, 6, 7);
         const bf16x8 vf = __builtin_bit_cast(bf16x8, c);
-        // P was packed by the previous phase B's softmax, a whole phase A (32 MFMAs) earlier, so no VALU -> MFMA
-        // hazard is left and it is read in place: the NOP form's "+v" operand made hipcc copy each group's P into
-        // a scratch register pair first (2 v_mov_b64 + s_nop per group)
+        // P was packed by the softmax before the barrier / the fenced read-ahead block above (and, inside the key
+        // loop, a whole phase A earlier): attn_common.h mfma_o's invariant, so it is read in place -- the NOP
+        // form's "+v" operand made hipcc copy each group's P into a scratch register pair (2 v_mov_b64 + s_nop)
         bf16x8 pk = __builtin_bit_cast(bf16x8, pc[g]);
         mfma_o<false>(o_acc[dt], vf, pk);
         __builtin_amdgcn_sched_barrier(0);

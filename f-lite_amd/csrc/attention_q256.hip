@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <queue>
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(NT, 1) void attn_q256_kernel(Q256Params P) {
   using BF = std::integral_constant<bool, false>;
   constexpr int KAHEAD = 2;  // K (+ block-1 Q) fragments read this many k-steps ahead
   constexpr int VAHEAD = 2;  // V^T fragments read this many fragments (= 4 MFMAs) ahead
+  static_assert(VAHEAD >= 1, "attn_common.h mfma_o: the read-ahead block separates the softmax from the PV MFMAs");
   f32x16 s0, s1;             // S^T of the pending tile: query block 0 / 1
   u32x4 pa[4], pb[4];        // P^T operands [qb * 2 + 16-key step] of two consecutive tiles, bf16 pairs
 
@@ -688,73 +690,92 @@ Plan make_plan(int cus, int pairs, int max_q, int max_k) {
   return pl;
 }
 
+// Route state: the mode and key floor are atomics set once from the environment (std::call_once) and by
+// flite_attn_set_q256; the kernel attribute and the CU count are per device; plans are cached per (CUs, pairs,
+// max_q, max_k) under g_plan_mu, and the cache is cleared past kMaxPlans entries (a varlen caller whose lengths
+// change every batch would otherwise grow it without bound; a plan is rebuilt in well under a millisecond).
 std::mutex g_plan_mu;
 std::map<std::tuple<int, int, int, int>, Plan> g_plans;
-bool g_q256_attr = false;
-int g_q256_cus = 0;
-int g_q256_mode = 2;  // 0 never, 1 always, 2 by the plan's prediction
-int g_min_keys = MIN_KEYS;
+constexpr size_t kMaxPlans = 256;
+std::map<int, int> g_dev_cus;  // device -> CU count, present once the attribute is set on that device
+std::once_flag g_env_once;
+std::atomic<int> g_q256_mode{2};  // 0 never, 1 always, 2 by the plan's prediction
+std::atomic<int> g_min_keys{MIN_KEYS};
 
+// the CU count of the current device (0 on failure), setting the kernel attribute there on first use
 int q256_init() {
-  if (g_q256_attr) return 0;
-  FLITE_HIP_CHECK(
-      hipFuncSetAttribute((const void*)attn_q256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+  std::call_once(g_env_once, [] {
+    // route policy: by default a launch takes the 256-row kernel where its split plan is predicted
+    // >= 4.5 % faster than the 128-row kernel's schedule (the 1344x896 self-attention, T = 4720: 465 vs 495 us
+    // measured; not at 1024^2, T = 4112, whose 768 128-row q-tiles are exactly 3 rounds of 256 CUs: 401 vs 375 us).
+    // FLITE_ATTN_Q256=1 / 0 or flite_attn_set_q256(1 / 0): always / never (the tests and A/B tools)
+    const char* on = getenv("FLITE_ATTN_Q256");
+    g_q256_mode = !on ? 2 : on[0] == '1' ? 1 : 0;
+    if (const char* mk = getenv("FLITE_Q256_MIN_KEYS")) g_min_keys = std::max(KT, atoi(mk));  // A/B: key-range floor
+  });
   int dev = 0;
-  FLITE_HIP_CHECK(hipGetDevice(&dev));
-  FLITE_HIP_CHECK(hipDeviceGetAttribute(&g_q256_cus, hipDeviceAttributeMultiprocessorCount, dev));
-  // route policy: by default a launch takes the 256-row kernel where its split plan is predicted >= 4.5 %
-  // faster than the 128-row kernel's schedule (the 1344x896 self-attention, T = 4720: 465 vs 495 us measured; not
-  // at 1024^2, T = 4112, whose 768 128-row q-tiles are exactly 3 rounds of 256 CUs: 401 vs 375 us). FLITE_ATTN_Q256=1
-  // / 0 or flite_attn_set_q256(1 / 0): always / never (the tests and A/B tools)
-  const char* on = getenv("FLITE_ATTN_Q256");
-  g_q256_mode = !on ? 2 : on[0] == '1' ? 1 : 0;
-  if (const char* mk = getenv("FLITE_Q256_MIN_KEYS")) g_min_keys = std::max(KT, atoi(mk));  // A/B: key-range floor
-  g_q256_attr = true;
-  return 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> g(g_plan_mu);
+  auto it = g_dev_cus.find(dev);
+  if (it != g_dev_cus.end()) return it->second;
+  int cus = 0;
+  if (hipFuncSetAttribute((const void*)attn_q256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  g_dev_cus[dev] = cus;
+  return cus;
 }
 
-const Plan* plan_for(int pairs, int max_q, int max_k) {
-  if (q256_init()) return nullptr;
+// the plan for this launch shape on the current device (copied out: the cache may be cleared by another thread)
+bool plan_for(int pairs, int max_q, int max_k, Plan* out) {
+  const int cus = q256_init();
+  if (cus <= 0) return false;
   std::lock_guard<std::mutex> g(g_plan_mu);
-  const auto key = std::make_tuple(g_q256_cus, pairs, max_q, max_k);
+  const auto key = std::make_tuple(cus, pairs, max_q, max_k);
   auto it = g_plans.find(key);
-  if (it == g_plans.end()) it = g_plans.emplace(key, make_plan(g_q256_cus, pairs, max_q, max_k)).first;
-  return &it->second;
+  if (it == g_plans.end()) {
+    if (g_plans.size() >= kMaxPlans) g_plans.clear();
+    it = g_plans.emplace(key, make_plan(cus, pairs, max_q, max_k)).first;
+  }
+  *out = it->second;
+  return true;
 }
 
 }  // namespace
 
 int attn_q256_set(int mode) {
-  if (q256_init()) return 1;
+  q256_init();  // the environment's choice is read first, so this call wins over it
   g_q256_mode = mode < 0 ? 0 : mode > 2 ? 2 : mode;
   return 0;
 }
 
 bool attn_q256_eligible(const AttnParams& p) {
-  if (q256_init() || g_q256_mode == 0) return false;
+  if (q256_init() <= 0 || g_q256_mode == 0) return false;
   return p.head_dim == HD && p.max_score > 0.f && p.part_mode == 0 && !p.k_end && p.split_ws &&
          p.max_q >= QT && p.max_k >= g_min_keys && p.B * p.H * (p.max_q / QT) <= (int)(CNT_BYTES / 4) - p.B * p.H;
 }
 
 long attn_q256_workspace_bytes(int B, int H, int max_q, int max_k) {
-  if (q256_init() || max_q < QT || max_k < g_min_keys) return 0;
+  if (q256_init() <= 0 || max_q < QT || max_k < g_min_keys) return 0;
   // launches past the counter block never take this route (attn_q256_eligible): no plan, no slabs
   if ((long)B * H * (max_q / QT) > (long)(CNT_BYTES / 4) - (long)B * H) return 0;
-  const Plan* pl = plan_for(B * H, max_q, max_k);
-  return pl ? pl->ws_bytes : 0;
+  Plan pl;
+  return plan_for(B * H, max_q, max_k, &pl) ? pl.ws_bytes : 0;
 }
 
 // attn_fwd's route for eligible launches whose workspace holds the plan's slabs; returns -1 when it does not apply
 int attn_q256_fwd(const AttnParams& p, hipStream_t stream) {
   if (!attn_q256_eligible(p)) return -1;
-  const Plan* pl = plan_for(p.B * p.H, p.max_q, p.max_k);
-  if (!pl || pl->ws_bytes > p.split_ws_bytes || (g_q256_mode == 2 && !pl->wins)) return -1;
+  Plan pl;
+  if (!plan_for(p.B * p.H, p.max_q, p.max_k, &pl) || pl.ws_bytes > p.split_ws_bytes || (g_q256_mode == 2 && !pl.wins))
+    return -1;
   Q256Params q;
   q.a = p;
   q.n_main = p.max_q / QT;
-  q.n_whole = pl->n_whole;
-  q.n_half = pl->n_half;
-  q.n_tail = pl->n_tail;
+  q.n_whole = pl.n_whole;
+  q.n_half = pl.n_half;
+  q.n_tail = pl.n_tail;
   const int pairs = p.B * p.H;
   dim3 grid(q.n_whole + 2 * q.n_half + pairs * q.n_tail);
   hipLaunchKernelGGL(attn_q256_kernel, grid, dim3(NT), LDS_BYTES, stream, q);

@@ -43,9 +43,14 @@ __device__ __forceinline__ void blds16(const i32x4& rsrc, unsigned voff, unsigne
 // O^T += V^T . P^T with the accumulator pinned to AGPRs. Left to itself hipcc keeps O (128 registers per lane)
 // in VGPRs inside the key loop and copies it to and from AGPRs every tile (~300 v_accvgpr moves per tile,
 // an issue-bound loop). An MFMA reads its srcC from AGPRs directly. The asm is opaque to the hazard
-// recognizer, so: the first MFMA after the VALU that produced its P operand carries `s_nop 1` (VALU write ->
-// MFMA read), and every reader of O after the loop waits behind o_acc_fence() (MFMA write -> read).
-// The NOP form also "redefines" pk, so every other MFMA reading pk is ordered after it.
+// recognizer, so the VALU write -> MFMA srcA/B read distance of the P operand must hold by construction. Both
+// kernels use only the no-NOP form, under this invariant: every P register is written by the softmax VALU before
+// a workgroup barrier or a sched_barrier(0)-fenced block of at least VAHEAD transposed V reads (two ds_read each;
+// VAHEAD >= 1 is static_asserted at each kernel), all issued before the first PV MFMA that reads it. In the key
+// loop a whole phase A (32 MFMAs) also lies in between; on the last tile (no phase A) and on the single-tile path
+// (prologue softmax, barrier, phase B) the barrier and the read-ahead block alone provide the distance. Every
+// reader of O after the loop waits behind o_acc_fence() (MFMA write -> read). The NOP form (`s_nop 1`, and a
+// "+v" pk that orders later readers after it) is kept for a P produced right before its MFMA.
 template <bool NOP>
 __device__ __forceinline__ void mfma_o(f32x16& acc, const bf16x8& v, bf16x8& pk) {
   if constexpr (NOP)

@@ -496,6 +496,24 @@ int flite_dit_set_fp8_gemm_classes(flite_dit* dit, int mask) {
   return dit->eng->set_fp8_classes(mask);
 }
 
+int flite_dit_set_fp8_block_classes(flite_dit* dit, const int* masks, int n_blocks) {
+  FLITE_REQUIRE(dit, "flite_dit_set_fp8_block_classes: null engine");
+  return dit->eng->set_fp8_block_classes(masks, n_blocks);
+}
+
+int flite_dit_set_residual_bf16(flite_dit* dit, int enable) {
+  FLITE_REQUIRE(dit, "flite_dit_set_residual_bf16: null engine");
+  return dit->eng->set_residual_bf16(enable != 0);
+}
+
+int flite_dit_residual_bf16(flite_dit* dit) {
+  if (!dit) {
+    set_last_error("flite: flite_dit_residual_bf16: null engine");
+    return -1;
+  }
+  return dit->eng->residual_bf16() ? 1 : 0;
+}
+
 int flite_dit_weights_updated(flite_dit* dit, void* stream) {
   FLITE_REQUIRE(dit, "flite_dit_weights_updated: null engine");
   return dit->eng->weights_updated((hipStream_t)stream);

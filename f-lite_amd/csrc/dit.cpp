@@ -70,6 +70,8 @@ DitEngine::DitEngine(const flite_dit_config& c) : cfg(c) {
   P = c.patch_size;
   C = c.in_channels;
   w_.blocks.resize(c.depth);
+  const char* x16 = getenv("FLITE_RESID_BF16");  // the residual-stream storage default (A/B switch)
+  x16_ = x16 != nullptr && x16[0] == '1';
   for (int i = 0; i < c.depth; ++i)
     w_.blocks[i].cross = c.per_block_adaln ? true : (i % 4 == 0 || i < 8);  // model.py:464 / model_v2.py:468
 }
@@ -590,7 +592,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     nm.in_seg = Tl_;
     nm.in_stride = Tl_;
     nm.in_off = 0;
-    return rmsnorm_mod(nm, false, s);
+    return rmsnorm_mod(nm, x16_, s);
   };
   auto resid = [&](const bf16_t* A, long lda, const bf16_t* W, int K, const float* gate, long rows = 0) -> int {
     GemmParams g;
@@ -606,7 +608,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     g.M = (int)(rows > 0 ? rows : M_);
     g.N = D;
     g.K = K;
-    return gemm(g, EPI_RESID_F32, s);
+    return gemm(g, epi_resid(), s);
   };
   const long rope_off = (long)sp_rank_ * Tl_ * 128;  // table rows of the tokens held here
 
@@ -680,7 +682,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   }
   if (resid(obuf_, D, b.proj_w, D, gate_sa, Msa)) return 1;
   for (long r0 = Msa; r0 < M_; r0 += Msa)  // the other CFG copies of the residual rows
-    FLITE_HIP_CHECK(hipMemcpyAsync(x_ + r0 * D, x_, (size_t)Msa * D * sizeof(float), hipMemcpyDeviceToDevice, s));
+    FLITE_HIP_CHECK(hipMemcpyAsync(xrow(r0), x_, (size_t)Msa * D * xbytes(), hipMemcpyDeviceToDevice, s));
 
   // --- cross attention (model.py:291-297) ---
   // The first ctx_uni_ sequences have uniform context (set_context): their rows take the step-invariant
@@ -692,7 +694,8 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
   const long r0 = (long)U * Tl_;
   const bool bc_defer = U > 0 && D == 3072;
   const float* bc_c = bc_defer ? ctx_c_ + (long)blk * B_ * D : nullptr;
-  if (U > 0 && !bc_defer && ctx_bcast_resid(x_, ctx_c_ + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s)) return 1;
+  if (U > 0 && !bc_defer && ctx_bcast_resid(x_, x16_, ctx_c_ + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s))
+    return 1;
   if (b.cross && r0 < M_) {
     {
       NormModParams nm;
@@ -700,7 +703,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
         nm.pf[0] = b.cq_w;
         nm.pf_bytes[0] = (long)D * D * 2;
       }
-      nm.x = x_ + r0 * D;
+      nm.x = xrow(r0);
       nm.ldx = D;
       nm.y = nbuf_ + r0 * D;
       nm.ldy = D;
@@ -713,7 +716,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
       nm.in_seg = Tl_;
       nm.in_stride = Tl_;
       nm.in_off = 0;
-      if (rmsnorm_mod(nm, false, s)) return 1;
+      if (rmsnorm_mod(nm, x16_, s)) return 1;
     }
     GemmParams g;
     g.A = nbuf_ + r0 * D;
@@ -767,7 +770,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     c.lda = D;
     c.W = b.cproj_w;
     c.ldw = D;
-    c.out = x_ + r0 * D;
+    c.out = xrow(r0);
     c.ldo = D;
     c.gate = gate_ca + U * mseg;
     c.gate_seg_stride = mseg;
@@ -775,7 +778,7 @@ int DitEngine::run_block(hipStream_t s, int blk, const float* mod, long mseg) {
     c.M = (int)(M_ - r0);
     c.N = D;
     c.K = D;
-    if (gemm(c, EPI_RESID_F32, s)) return 1;
+    if (gemm(c, epi_resid(), s)) return 1;
   }
 
   // --- SwiGLU MLP (model.py:299-301) ---
@@ -857,6 +860,22 @@ int DitEngine::set_fp8_classes(int mask) {
   FLITE_REQUIRE(mask >= 0 && mask <= FLITE_FP8_ALL, "set_fp8_gemm_classes: mask outside FLITE_FP8_ALL");
   if (mask != fp8_classes_) drop_graph();  // a cached graph holds the old choice
   fp8_classes_ = mask;
+  return 0;
+}
+
+int DitEngine::set_fp8_block_classes(const int* masks, int n) {
+  FLITE_REQUIRE(n == 0 || (masks != nullptr && n == cfg.depth),
+                "set_fp8_block_classes: pass one mask per block (n = depth), or n = 0 to clear");
+  std::vector<int> m(masks, masks + n);
+  for (int v : m) FLITE_REQUIRE(v >= 0 && v <= FLITE_FP8_ALL, "set_fp8_block_classes: mask outside FLITE_FP8_ALL");
+  drop_graph();  // a cached graph holds the old per-block choice
+  fp8_blk_mask_.swap(m);
+  return 0;
+}
+
+int DitEngine::set_residual_bf16(bool on) {
+  if (on != x16_) drop_graph();  // a cached graph holds the other launch shapes
+  x16_ = on;
   return 0;
 }
 
@@ -946,7 +965,7 @@ int DitEngine::collapse_fp8(hipStream_t s) {
 
 // One DiTBlock in fp8 (flite_dit_enable_fp8): the six block GEMMs on MXFP8 operands; attention, RoPE / QK-norm,
 // the residual stream and the modulation stay as in run_block.
-int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg) {
+int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg, int cm) {
   const BlockW& b = w_.blocks[blk];
   const Fp8W& q = w8_[blk];
   const float *shift_sa = mod, *scale_sa = mod + D, *gate_sa = mod + 2L * D;
@@ -958,7 +977,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   auto norm8 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0, long r0 = 0,
                     const float* bc_c = nullptr, long bc_rows = 0) -> int {
     NormModParams nm;  // rows [r0, r0 + rows) of x; r0 % 4 == 0 keeps the scale rows 16-B aligned (uni_fp8)
-    nm.x = x_ + r0 * D;
+    nm.x = xrow(r0);
     nm.ldx = D;
     nm.y8 = nbuf8_ + r0 * D;
     nm.ldy = D;
@@ -978,7 +997,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     nm.bc_gate_stride = mseg;
     nm.bc_rows = bc_rows;
     nm.bc_rows_per_seg = Tl_;
-    return rmsnorm_mod(nm, false, s);
+    return rmsnorm_mod(nm, x16_, s);
   };
   auto g8 = [&](const uint8_t* A, const uint8_t* As, const uint8_t* W, const uint8_t* Ws, long w_rows, int N, int K,
                 const bf16_t* bias, int epi, void* out, long ldo, const float* gate, int norm_cols = 0,
@@ -1060,13 +1079,12 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   };
   // the GEMM classes on MXFP8 (flite_dit_set_fp8_gemm_classes); every other class runs its bf16 GEMM, and each
   // activation is produced in the format its consumer takes
-  const int cm = fp8_classes_;
   const bool f_qkv = cm & FLITE_FP8_QKV, f_proj = cm & FLITE_FP8_PROJ, f_cq = cm & FLITE_FP8_CROSS_Q,
              f_cproj = cm & FLITE_FP8_CROSS_PROJ, f_gu = cm & FLITE_FP8_GATE_UP, f_down = cm & FLITE_FP8_DOWN;
   auto norm16 = [&](const bf16_t* w, const float* sh, const float* sc, long rows = 0, long r0 = 0,
                     const float* bc_c = nullptr, long bc_rows = 0) -> int {
     NormModParams nm;
-    nm.x = x_ + r0 * D;
+    nm.x = xrow(r0);
     nm.ldx = D;
     nm.y = nbuf_ + r0 * D;
     nm.ldy = D;
@@ -1084,7 +1102,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     nm.bc_gate_stride = mseg;
     nm.bc_rows = bc_rows;
     nm.bc_rows_per_seg = Tl_;
-    return rmsnorm_mod(nm, false, s);
+    return rmsnorm_mod(nm, x16_, s);
   };
   auto g16 = [&](const bf16_t* A, const bf16_t* W, int N, const bf16_t* bias, int epi, void* out, long ldo,
                  const float* gate, int norm_cols = 0, int rope_cols = 0, long rows = 0) -> int {
@@ -1126,12 +1144,12 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   if (probe_sa && probe_end(s, FLITE_PROBE_ATTN_SELF)) return 1;
   if (f_proj) {
     if (!attn_mx_ && quant_rows_fp8(obuf_, D, Msa, D, obuf8_, D, obuf8_s_, mpad_, s)) return 1;
-    if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, EPI8_RESID_F32, x_, D, gate_sa, 0, 0, Msa)) return 1;
-  } else if (g16(obuf_, b.proj_w, D, nullptr, EPI_RESID_F32, x_, D, gate_sa, 0, 0, Msa)) {
+    if (g8(obuf8_, obuf8_s_, q.proj, q.proj_s, D, D, D, nullptr, epi8_resid(), x_, D, gate_sa, 0, 0, Msa)) return 1;
+  } else if (g16(obuf_, b.proj_w, D, nullptr, epi_resid(), x_, D, gate_sa, 0, 0, Msa)) {
     return 1;
   }
   for (long r0 = Msa; r0 < M_; r0 += Msa)  // the other CFG copies of the residual rows
-    FLITE_HIP_CHECK(hipMemcpyAsync(x_ + r0 * D, x_, (size_t)Msa * D * sizeof(float), hipMemcpyDeviceToDevice, s));
+    FLITE_HIP_CHECK(hipMemcpyAsync(xrow(r0), x_, (size_t)Msa * D * xbytes(), hipMemcpyDeviceToDevice, s));
   // --- cross attention --- (uniform-context collapse as in run_block: the first U sequences' rows take
   // x += gate_ca * c8, the rest run the sub-block from row r0 on)
   // (an MXFP8 cross-q or cross-proj keeps the collapsed rows' r0 16-B aligned in the scale arrays: uni_fp8; a bf16
@@ -1143,7 +1161,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   const bool bc_defer = U > 0 && D == 3072;
   const float* bc_c = bc_defer ? (f_cproj ? ctx_c8_ : ctx_c_) + (long)blk * B_ * D : nullptr;
   if (U > 0 && !bc_defer &&
-      ctx_bcast_resid(x_, (f_cproj ? ctx_c8_ : ctx_c_) + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s))
+      ctx_bcast_resid(x_, x16_, (f_cproj ? ctx_c8_ : ctx_c_) + (long)blk * B_ * D, gate_ca, mseg, Tl_, r0, D, s))
     return 1;
   if (b.cross && rows > 0) {
     if (f_cq ? norm8(b.norm2, shift_ca + U * mseg, scale_ca + U * mseg, rows, r0)
@@ -1164,10 +1182,10 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     if (f_cproj) {
       if (!attn_mx_ && quant_rows_fp8(obuf_ + r0 * D, D, rows, D, obuf8_ + r0 * D, D, obuf8_s_ + r0 * 4, mpad_, s))
         return 1;
-      if (g8(obuf8_ + r0 * D, obuf8_s_ + r0 * 4, q.cproj, q.cproj_s, D, D, D, nullptr, EPI8_RESID_F32, x_ + r0 * D, D,
+      if (g8(obuf8_ + r0 * D, obuf8_s_ + r0 * 4, q.cproj, q.cproj_s, D, D, D, nullptr, epi8_resid(), xrow(r0), D,
              gate_ca + U * mseg, 0, 0, rows))
         return 1;
-    } else if (g16(obuf_ + r0 * D, b.cproj_w, D, nullptr, EPI_RESID_F32, x_ + r0 * D, D, gate_ca + U * mseg, 0, 0,
+    } else if (g16(obuf_ + r0 * D, b.cproj_w, D, nullptr, epi_resid(), xrow(r0), D, gate_ca + U * mseg, 0, 0,
                    rows)) {
       return 1;
     }
@@ -1200,7 +1218,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
   if (probe_end(s, FLITE_PROBE_GEMM_GATEUP)) return 1;
   if (probe_begin(s, FLITE_PROBE_GEMM_DOWN)) return 1;
   if (f_down) {
-    if (g8(hbuf8_, hbuf8_s_, q.down, q.down_s, D, D, F, nullptr, EPI8_RESID_F32, x_, D, gate_mlp)) return 1;
+    if (g8(hbuf8_, hbuf8_s_, q.down, q.down_s, D, D, F, nullptr, epi8_resid(), x_, D, gate_mlp)) return 1;
   } else {
     GemmParams g;
     g.A = hbuf_;
@@ -1215,7 +1233,7 @@ int DitEngine::run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg
     g.M = (int)M_;
     g.N = D;
     g.K = F;
-    if (gemm(g, EPI_RESID_F32, s)) return 1;
+    if (gemm(g, epi_resid(), s)) return 1;
   }
   if (probe_end(s, FLITE_PROBE_GEMM_DOWN)) return 1;
   return 0;
@@ -1276,8 +1294,8 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     const int r0 = sp_rank_ * Tl_, t_hi = std::min(T_, r0 + Tl_);
     const int p0 = std::max(r0 - R, 0), p1 = t_hi - R;
     if (t_hi < r0 + Tl_)  // padding rows of the last rank: keep them finite
-      FLITE_HIP_CHECK(hipMemset2DAsync(x_ + (long)(t_hi - r0) * D, (size_t)Tl_ * D * 4, 0,
-                                       (size_t)(r0 + Tl_ - t_hi) * D * 4, B_, s));
+      FLITE_HIP_CHECK(hipMemset2DAsync(xrow(t_hi - r0), (size_t)Tl_ * D * xbytes(), 0,
+                                       (size_t)(r0 + Tl_ - t_hi) * D * xbytes(), B_, s));
     for (int b = 0; b < B_ && p1 > p0; ++b) {
       GemmParams g;
       g.A = patches_ + ((long)b * HW_ + p0) * cpp;
@@ -1285,14 +1303,14 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
       g.W = w_.patch_w;
       g.ldw = cpp;
       g.bias = w_.patch_b;
-      g.out = x_ + ((long)b * Tl_ + (p0 + R - r0)) * D;
+      g.out = xrow((long)b * Tl_ + (p0 + R - r0));
       g.ldo = D;
       g.M = p1 - p0;
       g.N = D;
       g.K = cpp;
-      if (gemm(g, EPI_STORE_F32, s)) return 1;
+      if (gemm(g, x16_ ? EPI_STORE_BF16 : EPI_STORE_F32, s)) return 1;
     }
-    if (r0 == 0 && fill_registers(x_, w_.registers, B_, Tl_, R, D, s)) return 1;
+    if (r0 == 0 && fill_registers(x_, x16_, w_.registers, B_, Tl_, R, D, s)) return 1;
   } else {
     GemmParams g;
     g.A = patches_;
@@ -1308,11 +1326,11 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     g.out_seg = HW_;
     g.out_seg_stride = T_;
     g.out_seg_off = R;
-    if (gemm(g, EPI_STORE_F32, s)) return 1;
-    if (fill_registers(x_, w_.registers, B_, T_, R, D, s)) return 1;
+    if (gemm(g, x16_ ? EPI_STORE_BF16 : EPI_STORE_F32, s)) return 1;
+    if (fill_registers(x_, x16_, w_.registers, B_, T_, R, D, s)) return 1;
   }
   // use_rope = False: x + positional_embedding[:, :T] over the register + patch rows (model.py:546)
-  if (!cfg.use_rope && add_pos_embed(x_, w_.pos_emb, B_, T_, D, s)) return 1;
+  if (!cfg.use_rope && add_pos_embed(x_, x16_, w_.pos_emb, B_, T_, D, s)) return 1;
   const long mseg = (long)t_row_step * mod_t_stride_;
   for (int i = 0; i < cfg.depth; ++i) {
     const float* mod = mod_ + (long)t_row0 * mod_t_stride_ + (cfg.per_block_adaln ? (long)i * 9 * D : 0);
@@ -1323,8 +1341,9 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     // cross-attention, so block 0's self-attention sub-block runs once per image instead of once per copy (one
     // rank; bf16 and MXFP8 paths)
     sa_seqs_ = (i == 0 && dup > 1 && t_row_step == 0 && sp_n_ == 1 && cfg_dedup()) ? Bi : 0;
-    const bool blk8 = fp8_ && fp8_classes_ != 0 && !(i < (int)fp8_bf16_blk_.size() && fp8_bf16_blk_[i]);
-    const int rc = blk8 ? run_block_fp8(s, i, mod, mseg) : run_block(s, i, mod, mseg);
+    const int cm = i < (int)fp8_blk_mask_.size() ? fp8_blk_mask_[i] : fp8_classes_;  // this block's MXFP8 classes
+    const bool blk8 = fp8_ && cm != 0 && !(i < (int)fp8_bf16_blk_.size() && fp8_bf16_blk_[i]);
+    const int rc = blk8 ? run_block_fp8(s, i, mod, mseg, cm) : run_block(s, i, mod, mseg);
     sa_seqs_ = 0;
     if (rc) return 1;
   }
@@ -1346,7 +1365,7 @@ int DitEngine::forward(hipStream_t s, const void* lat, bool lat_bf16, int Bi, in
     nm.in_seg = sp ? Tl_ : HW_;
     nm.in_stride = sp ? Tl_ : T_;
     nm.in_off = sp ? 0 : R;
-    if (rmsnorm_mod(nm, false, s)) return 1;
+    if (rmsnorm_mod(nm, x16_, s)) return 1;
     GemmParams g;
     g.A = nbuf_;
     g.lda = D;

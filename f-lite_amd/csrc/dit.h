@@ -52,6 +52,11 @@ class DitEngine {
   int enable_fp8(hipStream_t s, bool on);
   int set_fp8_bf16_blocks(const int* blocks, int n);
   int set_fp8_classes(int mask);
+  // per-block class masks (flite_dit_set_fp8_block_classes): n = depth masks, or n = 0 to use set_fp8_classes' one
+  int set_fp8_block_classes(const int* masks, int n);
+  // residual stream storage: fp32 (default) or bf16 (drops the cached graph)
+  int set_residual_bf16(bool on);
+  bool residual_bf16() const { return x16_; }
   // the bound weights' CONTENTS changed in place (flite_dit_weights_updated): requantise the fp8 copies
   int weights_updated(hipStream_t s);
 
@@ -81,7 +86,7 @@ class DitEngine {
   int sp_self_attention(hipStream_t s, AttnParams a);
   int sp_ring_attention(hipStream_t s, AttnParams a);
   int sp_gather_out(hipStream_t s);
-  int run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg);
+  int run_block_fp8(hipStream_t s, int blk, const float* mod, long mseg, int classes);
   int alloc_fp8_act();
   int quantise_fp8(hipStream_t s);
   void free_fp8_weights();
@@ -135,7 +140,14 @@ class DitEngine {
   int collapse_fp8(hipStream_t s);
   int uni_fp8() const;
   // workspace
-  float* x_ = nullptr;
+  // residual stream [M, D]: fp32, or bf16 with x16_ (flite_dit_set_residual_bf16; the reference's own storage type,
+  // model.py:289). Every writer is an fp32 fma with one rounding; the buffer is sized for fp32 either way.
+  void* x_ = nullptr;
+  bool x16_ = false;
+  size_t xbytes() const { return x16_ ? 2 : 4; }
+  void* xrow(long r) const { return (char*)x_ + r * (long)D * (long)xbytes(); }
+  int epi_resid() const { return x16_ ? EPI_RESID_BF16 : EPI_RESID_F32; }
+  int epi8_resid() const { return x16_ ? EPI8_RESID_BF16 : EPI8_RESID_F32; }
   bf16_t *nbuf_ = nullptr, *qkv_ = nullptr, *obuf_ = nullptr, *hbuf_ = nullptr, *patches_ = nullptr;
   float* fout_ = nullptr;
   float* acc_ = nullptr;  // graph-owned Euler accumulator (sample)
@@ -165,6 +177,7 @@ class DitEngine {
   bool fp8_ = false;
   std::vector<char> fp8_bf16_blk_;  // blocks that stay bf16 in fp8 mode (flite_dit_set_fp8_bf16_blocks)
   int fp8_classes_ = 63;            // GEMM classes on MXFP8 in the fp8 blocks (flite_dit_set_fp8_gemm_classes)
+  std::vector<int> fp8_blk_mask_;   // per-block classes (flite_dit_set_fp8_block_classes); empty = fp8_classes_
   bool w8_stale_ = true;  // the fp8 copies do not reflect the bound bf16 weights (requantised before the next use)
   bool ctx_stale_ = false;  // a weight changed after set_context: the cached context K/V are stale
   std::vector<Fp8W> w8_;

@@ -106,7 +106,8 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_kernel(NormModParams p) {
 // a wave reduction plus 4 partials through LDS.
 // PF: the weight read-ahead below is compiled in; the PF = false instantiation is the plain kernel (the
 // read-ahead's registers and loads had cost every launch ~8 us, round-2 VERDICT item 4).
-// BC: the deferred broadcast residual of NormModParams (bc_*), applied to the fp32 row before the reduction.
+// BC: the deferred broadcast residual of NormModParams (bc_*), applied to the row (fp32 or, IN_BF16, the bf16
+// residual stream) before the reduction.
 template <bool IN_BF16, int NQ, bool OUT8 = false, bool PF = false, bool BC = false>
 __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
   __shared__ float part[4];
@@ -124,6 +125,26 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
       v[4 * q + 1] = __uint_as_float(w.x & 0xffff0000u);
       v[4 * q + 2] = __uint_as_float(w.y << 16);
       v[4 * q + 3] = __uint_as_float(w.y & 0xffff0000u);
+    }
+    if constexpr (BC) {  // bf16 residual stream (DitEngine resid16): the same fma, one rounding, written back
+      if (m < p.bc_rows) {
+        const long bs = m / p.bc_rows_per_seg;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int n = q * 1024 + t * 4;
+          const f32x4 cv = *(const f32x4*)(p.bc_c + bs * (long)(1024 * NQ) + n);
+          const f32x4 gv = *(const f32x4*)(p.bc_gate + bs * p.bc_gate_stride + n);
+          float nv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) nv[j] = __builtin_fmaf(cv[j], gv[j], v[4 * q + j]);
+          const u32x2 st = {pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
+          *(u32x2*)((bf16_t*)p.x + in_row * p.ldx + n) = st;
+          v[4 * q + 0] = __uint_as_float(st.x << 16);  // normalise what the stream now holds
+          v[4 * q + 1] = __uint_as_float(st.x & 0xffff0000u);
+          v[4 * q + 2] = __uint_as_float(st.y << 16);
+          v[4 * q + 3] = __uint_as_float(st.y & 0xffff0000u);
+        }
+      }
     }
   } else {
     const float* xr = (const float*)p.x + in_row * p.ldx;
@@ -304,23 +325,31 @@ __global__ __launch_bounds__(256) void patchify_kernel(const void* lat, bf16_t* 
   }
 }
 
-// register tokens into rows [0, R) of every sequence of the fp32 residual stream
-__global__ __launch_bounds__(256) void fill_registers_kernel(float* x, const bf16_t* reg, int B, int T, int R,
-                                                             int D) {
+// register tokens into rows [0, R) of every sequence of the residual stream (fp32, or bf16 when X16)
+template <bool X16>
+__global__ __launch_bounds__(256) void fill_registers_kernel(void* x, const bf16_t* reg, int B, int T, int R, int D) {
   const long total = (long)B * R * D;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     const int d = (int)(idx % D);
     const long r = (idx / D) % R;
     const long b = idx / ((long)D * R);
-    x[(b * T + r) * D + d] = bf2f(reg[r * D + d]);
+    if constexpr (X16)
+      ((bf16_t*)x)[(b * T + r) * D + d] = reg[r * D + d];
+    else
+      ((float*)x)[(b * T + r) * D + d] = bf2f(reg[r * D + d]);
   }
 }
 
 // x[b][t] += positional_embedding[t] for every row t of every sample (use_rope = False, model.py:546)
-__global__ __launch_bounds__(256) void add_pos_embed_kernel(float* x, const bf16_t* pos, int B, int T, int D) {
+template <bool X16>
+__global__ __launch_bounds__(256) void add_pos_embed_kernel(void* x, const bf16_t* pos, int B, int T, int D) {
   const long total = (long)B * T * D;
-  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x)
-    x[idx] += bf2f(pos[idx % ((long)T * D)]);
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    if constexpr (X16)
+      ((bf16_t*)x)[idx] = f2bf(bf2f(((bf16_t*)x)[idx]) + bf2f(pos[idx % ((long)T * D)]));
+    else
+      ((float*)x)[idx] += bf2f(pos[idx % ((long)T * D)]);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -464,7 +493,9 @@ __global__ __launch_bounds__(256) void rows_uniform_kernel(const unsigned* x, lo
 // Collapsed rows r < rows (sequences whose cross-attention keys are all equal): the attention output of every such
 // row is the sequence's one V row, so the gated residual of its cross-proj is the step-invariant c[seq] = V.Wproj^T
 // (made once per set_context): x[r][n] += gate[seq][n] * c[seq][n] -- the cross-proj epilogue's own expression.
-__global__ __launch_bounds__(256) void ctx_bcast_resid_kernel(float* x, const float* c, const float* gate,
+// (X16: the bf16 residual stream, one rounding of the fp32 fma; rmsnorm_mod_row_kernel's BC form, bit for bit)
+template <bool X16>
+__global__ __launch_bounds__(256) void ctx_bcast_resid_kernel(void* x, const float* c, const float* gate,
                                                               long gate_seg_stride, int rows_per_seg, long rows,
                                                               int D) {
   const int d4 = D / 4;
@@ -473,12 +504,22 @@ __global__ __launch_bounds__(256) void ctx_bcast_resid_kernel(float* x, const fl
     const long r = i / d4;
     const int n = (int)(i - r * d4) * 4;
     const long seq = r / rows_per_seg;
-    f32x4 xv = *(const f32x4*)(x + r * D + n);
+    f32x4 xv;
+    if constexpr (X16) {
+      const u32x2 w = *(const u32x2*)((const bf16_t*)x + r * D + n);
+      xv = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u), __uint_as_float(w.y << 16),
+                 __uint_as_float(w.y & 0xffff0000u)};
+    } else {
+      xv = *(const f32x4*)((const float*)x + r * D + n);
+    }
     const f32x4 cv = *(const f32x4*)(c + seq * D + n);
     const f32x4 gv = *(const f32x4*)(gate + seq * gate_seg_stride + n);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) xv[j] += cv[j] * gv[j];
-    *(f32x4*)(x + r * D + n) = xv;
+    for (int j = 0; j < 4; ++j) xv[j] = __builtin_fmaf(cv[j], gv[j], xv[j]);
+    if constexpr (X16)
+      *(u32x2*)((bf16_t*)x + r * D + n) = u32x2{pack2bf(xv[0], xv[1]), pack2bf(xv[2], xv[3])};
+    else
+      *(f32x4*)((float*)x + r * D + n) = xv;
   }
 }
 
@@ -637,27 +678,40 @@ int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   FLITE_REQUIRE(p.bc_rows <= 0 || (p.D == 3072 && p.rows < (1L << 31)),
                 "rmsnorm: the deferred broadcast residual is implemented for the D = 3072 row kernel only");
   if (p.rows <= 0) return 0;
-  if (p.y8 != nullptr) {  // MXFP8 output (fp8 DiT path): fp32 input rows only
-    FLITE_REQUIRE(!in_bf16 && p.ysc != nullptr && p.ysc_rows_pad >= mx_rows_pad(p.rows) && p.D % 128 == 0 &&
-                      p.ldy % 16 == 0,
-                  "rmsnorm(fp8 out): fp32 input, scales for the padded rows, D % 128, 16-B row stride");
+  if (p.y8 != nullptr) {  // MXFP8 output (fp8 DiT path): fp32 or bf16 residual rows
+    FLITE_REQUIRE(p.ysc != nullptr && p.ysc_rows_pad >= mx_rows_pad(p.rows) && p.D % 128 == 0 && p.ldy % 16 == 0,
+                  "rmsnorm(fp8 out): scales for the padded rows, D % 128, 16-B row stride");
     if (p.D == 3072) {
       if (p.bc_rows > 0) {
         FLITE_REQUIRE(p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
-                      "rmsnorm(fp8 out): the deferred broadcast residual needs fp32 rows in place");
-        hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, true, false, true>), dim3((unsigned)p.rows), dim3(256), 0,
-                           s, p);
+                      "rmsnorm(fp8 out): the deferred broadcast residual needs the rows in place");
+        if (in_bf16)
+          hipLaunchKernelGGL((rmsnorm_mod_row_kernel<true, 3, true, false, true>), dim3((unsigned)p.rows), dim3(256),
+                             0, s, p);
+        else
+          hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, true, false, true>), dim3((unsigned)p.rows), dim3(256),
+                             0, s, p);
+      } else if (in_bf16) {
+        hipLaunchKernelGGL((rmsnorm_mod_row_kernel<true, 3, true>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
       } else {
         hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, true>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
       }
     } else {
       const int grid8 = (int)((p.rows + 3) / 4);
+#define FLITE_NORM8_CASE(N)                                                                        \
+  case N:                                                                                           \
+    if (in_bf16)                                                                                    \
+      hipLaunchKernelGGL((rmsnorm_mod_kernel<true, N, true>), dim3(grid8), dim3(256), 0, s, p);     \
+    else                                                                                            \
+      hipLaunchKernelGGL((rmsnorm_mod_kernel<false, N, true>), dim3(grid8), dim3(256), 0, s, p);    \
+    break;
       switch (p.D / 256) {
-        case 1: hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 1, true>), dim3(grid8), dim3(256), 0, s, p); break;
-        case 2: hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 2, true>), dim3(grid8), dim3(256), 0, s, p); break;
-        case 4: hipLaunchKernelGGL((rmsnorm_mod_kernel<false, 4, true>), dim3(grid8), dim3(256), 0, s, p); break;
+        FLITE_NORM8_CASE(1)
+        FLITE_NORM8_CASE(2)
+        FLITE_NORM8_CASE(4)
         default: FLITE_REQUIRE(false, "rmsnorm(fp8 out): D must be 256, 512, 1024 or 3072");
       }
+#undef FLITE_NORM8_CASE
     }
     FLITE_HIP_CHECK(hipGetLastError());
     return 0;
@@ -665,12 +719,17 @@ int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   if (p.D == 3072 && p.rows < (1L << 31)) {  // the DiT width: one workgroup per row
     const bool pf = p.pf[0] != nullptr || p.pf[1] != nullptr;
     if (p.bc_rows > 0) {
-      FLITE_REQUIRE(!in_bf16 && !pf && p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate &&
-                        p.bc_rows_per_seg > 0,
-                    "rmsnorm: the deferred broadcast residual needs fp32 rows in place, no read-ahead");
-      hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, false, false, true>), dim3((unsigned)p.rows), dim3(256), 0,
-                         s, p);
-    } else if (in_bf16)
+      FLITE_REQUIRE(!pf && p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
+                    "rmsnorm: the deferred broadcast residual needs the rows in place, no read-ahead");
+      if (in_bf16)
+        hipLaunchKernelGGL((rmsnorm_mod_row_kernel<true, 3, false, false, true>), dim3((unsigned)p.rows), dim3(256), 0,
+                           s, p);
+      else
+        hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, false, false, true>), dim3((unsigned)p.rows), dim3(256),
+                           0, s, p);
+    } else if (in_bf16 && pf)
+      hipLaunchKernelGGL((rmsnorm_mod_row_kernel<true, 3, false, true>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
+    else if (in_bf16)
       hipLaunchKernelGGL((rmsnorm_mod_row_kernel<true, 3>), dim3((unsigned)p.rows), dim3(256), 0, s, p);
     else if (pf)
       hipLaunchKernelGGL((rmsnorm_mod_row_kernel<false, 3, false, true>), dim3((unsigned)p.rows), dim3(256), 0, s,
@@ -729,15 +788,24 @@ int patchify(const void* lat, bool in_bf16, bf16_t* out, int Bi, int C, int H, i
   return 0;
 }
 
-int fill_registers(float* x, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s) {
-  hipLaunchKernelGGL(fill_registers_kernel, dim3(grid_for((long)B * R * D)), dim3(256), 0, s, x, reg, B, T, R, D);
+int fill_registers(void* x, bool x16, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s) {
+  if (x16)
+    hipLaunchKernelGGL(fill_registers_kernel<true>, dim3(grid_for((long)B * R * D)), dim3(256), 0, s, x, reg, B, T,
+                       R, D);
+  else
+    hipLaunchKernelGGL(fill_registers_kernel<false>, dim3(grid_for((long)B * R * D)), dim3(256), 0, s, x, reg, B, T,
+                       R, D);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }
 
-int add_pos_embed(float* x, const bf16_t* pos, int B, int T, int D, hipStream_t s) {
+int add_pos_embed(void* x, bool x16, const bf16_t* pos, int B, int T, int D, hipStream_t s) {
   FLITE_REQUIRE(pos != nullptr, "add_pos_embed: positional_embedding not bound");
-  hipLaunchKernelGGL(add_pos_embed_kernel, dim3(grid_for((long)B * T * D)), dim3(256), 0, s, x, pos, B, T, D);
+  if (x16)
+    hipLaunchKernelGGL(add_pos_embed_kernel<true>, dim3(grid_for((long)B * T * D)), dim3(256), 0, s, x, pos, B, T, D);
+  else
+    hipLaunchKernelGGL(add_pos_embed_kernel<false>, dim3(grid_for((long)B * T * D)), dim3(256), 0, s, x, pos, B, T,
+                       D);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -773,12 +841,16 @@ int rows_uniform(const void* x, int cols, const int* cu, int nseq, int* bad, hip
   return 0;
 }
 
-int ctx_bcast_resid(float* x, const float* c, const float* gate, long gate_seg_stride, int rows_per_seg, long rows,
-                    int D, hipStream_t s) {
+int ctx_bcast_resid(void* x, bool x16, const float* c, const float* gate, long gate_seg_stride, int rows_per_seg,
+                    long rows, int D, hipStream_t s) {
   if (rows <= 0) return 0;
   FLITE_REQUIRE(D % 4 == 0, "ctx_bcast_resid: D must be a multiple of 4");
-  hipLaunchKernelGGL(ctx_bcast_resid_kernel, dim3(grid_for(rows * (D / 4))), dim3(256), 0, s, x, c, gate,
-                     gate_seg_stride, rows_per_seg, rows, D);
+  if (x16)
+    hipLaunchKernelGGL(ctx_bcast_resid_kernel<true>, dim3(grid_for(rows * (D / 4))), dim3(256), 0, s, x, c, gate,
+                       gate_seg_stride, rows_per_seg, rows, D);
+  else
+    hipLaunchKernelGGL(ctx_bcast_resid_kernel<false>, dim3(grid_for(rows * (D / 4))), dim3(256), 0, s, x, c, gate,
+                       gate_seg_stride, rows_per_seg, rows, D);
   FLITE_HIP_CHECK(hipGetLastError());
   return 0;
 }

@@ -29,6 +29,7 @@ __device__ __forceinline__ unsigned pack4_fp8(const float* x, float inv) {
 enum GemmFp8Epilogue {
   EPI8_STORE_BF16 = 0,  // out_bf16[m][n] = acc + bias[n]
   EPI8_RESID_F32 = 2,   // out_f32[m][n] += gate[seg(m)][n] * (acc + bias[n])
+  EPI8_RESID_BF16 = 7,  // the same on a bf16 residual stream: fp32 math, one rounding (gemm.hip EPI_RESID_BF16)
   EPI8_SWIGLU_FP8 = 4,  // W8 = gate|up interleaved in 16-row sub-tiles (N = 2F): out8[m][f] = MX(silu(g) * u),
                         // scales to out_sc [F/128][out_rows_pad][4]
   EPI8_QKV_NORM_BF16 = 5,  // engine-internal: bf16 store with RoPE + QK-norm of columns [0, norm_cols) (gemm.hip)

@@ -393,7 +393,9 @@ struct GemmCta {
   // the fp32 residual: the loads of two accumulator rows (8 x + 8 gate, 16 B per lane) are issued together at
   // clamped, always-valid addresses and only the stores are masked, so the tile pays 4 memory round trips
   // instead of one per 16-B group (a bounds branch around each load makes hipcc wait vmcnt(0) per group).
-  template <bool GATED, bool TWO_SEG>
+  // X16 (EPI_RESID_BF16): the residual stream is bf16, 8 B per 4 columns each way; the same fp32 expression, one
+  // rounding at the store.
+  template <bool GATED, bool TWO_SEG, bool X16 = false>
   __device__ __forceinline__ void resid_epilogue(const f32x4 (&acc)[8][4], int m_base, int n_base) {
     float bias[4][4];
     int nc[4];
@@ -424,19 +426,26 @@ struct GemmCta {
 #pragma unroll
     for (int mb = 0; mb < 8; mb += 2) {
       f32x4 xv[2][4], gv[2][4];
-      float* orow[2];
+      char* orow[2];
       bool mok[2];
+      constexpr int XB = X16 ? 2 : 4;  // bytes per residual element
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int m = m_base + (mb + i) * 16;
         mok[i] = mb + i < MI && m < p.M;
         const int mc = mok[i] ? m : p.M - 1;
-        orow[i] = (float*)p.out + (long)mc * p.ldo;
+        orow[i] = (char*)p.out + (long)mc * p.ldo * XB;
         const int seg = GATED ? mc / p.rows_per_seg : 0;
         const float* grow = GATED ? p.gate + (long)seg * p.gate_seg_stride : nullptr;
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
-          xv[i][ni] = *(const f32x4*)(orow[i] + nc[ni]);
+          if constexpr (X16) {
+            const u32x2 w = *(const u32x2*)(orow[i] + nc[ni] * XB);
+            xv[i][ni] = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                              __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+          } else {
+            xv[i][ni] = *(const f32x4*)(orow[i] + nc[ni] * XB);
+          }
           if constexpr (TWO_SEG)
             gv[i][ni] = seg == seg_lo ? g2[0][ni] : g2[1][ni];
           else if constexpr (GATED)
@@ -456,7 +465,11 @@ struct GemmCta {
             else
               x[r] += v;
           }
-          if (mok[i] && nok[ni]) *(f32x4*)(orow[i] + nc[ni]) = x;
+          if constexpr (X16) {
+            if (mok[i] && nok[ni]) *(u32x2*)(orow[i] + nc[ni] * XB) = u32x2{pack2bf(x[0], x[1]), pack2bf(x[2], x[3])};
+          } else {
+            if (mok[i] && nok[ni]) *(f32x4*)(orow[i] + nc[ni] * XB) = x;
+          }
         }
     }
   }
@@ -589,13 +602,14 @@ struct GemmCta {
         }
       }
       return;
-    } else if constexpr (EPI == EPI_RESID_F32) {
+    } else if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_RESID_BF16) {
+      constexpr bool X16 = EPI == EPI_RESID_BF16;
       if (p.gate == nullptr)
-        resid_epilogue<false, false>(acc, m_base, n_base);
+        resid_epilogue<false, false, X16>(acc, m_base, n_base);
       else if (p.rows_per_seg >= MI * 16)
-        resid_epilogue<true, true>(acc, m_base, n_base);
+        resid_epilogue<true, true, X16>(acc, m_base, n_base);
       else
-        resid_epilogue<true, false>(acc, m_base, n_base);
+        resid_epilogue<true, false, X16>(acc, m_base, n_base);
       return;
     } else {
       float bias[4][4];
@@ -787,6 +801,7 @@ int gemm_init() {
   FLITE_HIP_CHECK(set_attrs<EPI_STORE_BF16>());
   FLITE_HIP_CHECK(set_attrs<EPI_STORE_F32>());
   FLITE_HIP_CHECK(set_attrs<EPI_RESID_F32>());
+  FLITE_HIP_CHECK(set_attrs<EPI_RESID_BF16>());
   FLITE_HIP_CHECK(set_attrs<EPI_SWIGLU_BF16>());
   FLITE_HIP_CHECK(set_attrs<EPI_GEGLU_BF16>());
   FLITE_HIP_CHECK(set_attrs<EPI_QKV_NORM_BF16>());
@@ -850,6 +865,13 @@ int gemm_bf16(const GemmParams& p, int epi, hipStream_t stream) {
       FLITE_REQUIRE(p.gate == nullptr || p.rows_per_seg > 0, "gemm(resid): rows_per_seg must be > 0");
       FLITE_REQUIRE(p.out_seg == 0 && p.act == 0, "gemm(resid): no row remap or activation");
       launch<EPI_RESID_F32>(p, stream);
+      break;
+    case EPI_RESID_BF16:
+      FLITE_REQUIRE(p.N % 4 == 0 && p.ldo % 4 == 0 && ((uintptr_t)p.out & 7) == 0,
+                    "gemm(resid bf16): N, ldo multiples of 4, 8-B aligned rows");
+      FLITE_REQUIRE(p.gate == nullptr || p.rows_per_seg > 0, "gemm(resid): rows_per_seg must be > 0");
+      FLITE_REQUIRE(p.out_seg == 0 && p.act == 0, "gemm(resid): no row remap or activation");
+      launch<EPI_RESID_BF16>(p, stream);
       break;
     case EPI_QKV_NORM_BF16:
       FLITE_REQUIRE(p.N % 256 == 0 && p.ldo % 4 == 0 && p.norm_cols % 256 == 0 && p.rope_cols % 256 == 0 &&

@@ -436,7 +436,9 @@ struct Fp8Cta {
         }
       }
       return;
-    } else if constexpr (EPI == EPI8_RESID_F32) {
+    } else if constexpr (EPI == EPI8_RESID_F32 || EPI == EPI8_RESID_BF16) {
+      constexpr bool X16 = EPI == EPI8_RESID_BF16;  // bf16 residual stream: one rounding at the store
+      constexpr int XB = X16 ? 2 : 4;
       float bias[4][4];
       int nc[4];
       bool nok[4];
@@ -451,18 +453,24 @@ struct Fp8Cta {
 #pragma unroll
       for (int mb = 0; mb < 8; mb += 2) {
         f32x4 xv[2][4], gv[2][4];
-        float* orow[2];
+        char* orow[2];
         bool mok[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int m = m_base + (mb + i) * 16;
           mok[i] = mb + i < MI && m < p.M;
           const int mc = mok[i] ? m : p.M - 1;
-          orow[i] = (float*)p.out + (long)mc * p.ldo;
+          orow[i] = (char*)p.out + (long)mc * p.ldo * XB;
           const float* grow = p.gate + (long)(mc / p.rows_per_seg) * p.gate_seg_stride;
 #pragma unroll
           for (int ni = 0; ni < 4; ++ni) {
-            xv[i][ni] = *(const f32x4*)(orow[i] + nc[ni]);
+            if constexpr (X16) {
+              const u32x2 w = *(const u32x2*)(orow[i] + nc[ni] * XB);
+              xv[i][ni] = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                                __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+            } else {
+              xv[i][ni] = *(const f32x4*)(orow[i] + nc[ni] * XB);
+            }
             gv[i][ni] = p.gate ? *(const f32x4*)(grow + nc[ni]) : f32x4{1.f, 1.f, 1.f, 1.f};
           }
         }
@@ -473,7 +481,11 @@ struct Fp8Cta {
             f32x4 x = xv[i][ni];
 #pragma unroll
             for (int r = 0; r < 4; ++r) x[r] += (acc[mb + i][ni][r] + bias[ni][r]) * gv[i][ni][r];
-            if (mok[i] && nok[ni]) *(f32x4*)(orow[i] + nc[ni]) = x;
+            if constexpr (X16) {
+              if (mok[i] && nok[ni]) *(u32x2*)(orow[i] + nc[ni] * XB) = u32x2{pack2bf(x[0], x[1]), pack2bf(x[2], x[3])};
+            } else {
+              if (mok[i] && nok[ni]) *(f32x4*)(orow[i] + nc[ni] * XB) = x;
+            }
           }
       }
       return;
@@ -558,6 +570,7 @@ int init8() {
   if (g_attrs) return 0;
   FLITE_HIP_CHECK(set_attrs8<EPI8_STORE_BF16>());
   FLITE_HIP_CHECK(set_attrs8<EPI8_RESID_F32>());
+  FLITE_HIP_CHECK(set_attrs8<EPI8_RESID_BF16>());
   FLITE_HIP_CHECK(set_attrs8<EPI8_SWIGLU_FP8>());
   FLITE_HIP_CHECK(set_attrs8<EPI8_QKV_NORM_BF16>());
   FLITE_HIP_CHECK(set_attrs8<EPI8_SWIGLU_BF16>());
@@ -628,6 +641,11 @@ int gemm_fp8(const GemmFp8Params& p, int epi, hipStream_t s) {
     case EPI8_RESID_F32:
       FLITE_REQUIRE(p.N % 4 == 0 && p.ldo % 4 == 0 && p.rows_per_seg > 0, "gemm_fp8(resid): N, ldo, rows_per_seg");
       launch8<EPI8_RESID_F32>(p, s);
+      break;
+    case EPI8_RESID_BF16:
+      FLITE_REQUIRE(p.N % 4 == 0 && p.ldo % 4 == 0 && p.rows_per_seg > 0 && ((uintptr_t)p.out & 7) == 0,
+                    "gemm_fp8(resid bf16): N, ldo, rows_per_seg, 8-B aligned rows");
+      launch8<EPI8_RESID_BF16>(p, s);
       break;
     case EPI8_SWIGLU_FP8:
       FLITE_REQUIRE(p.N % 256 == 0, "gemm_fp8(swiglu): 2F must be a multiple of 256");

@@ -12,6 +12,8 @@ enum GemmEpilogue {
   EPI_GEGLU_BF16 = 6,   // out_bf16[m][f] = gelu_tanh(A.Wg[f]) * (A.Wu[f])     (T5 DenseGatedActDense wi_0 / wi_1)
   EPI_QKV_NORM_BF16 = 5,  // out_bf16 = acc + bias; columns [0, norm_cols) (heads of 256) first get 2-D RoPE
                           // (columns [0, rope_cols)) and QKNorm's per-head RMSNorm (model.py:166-180,197)
+  EPI_RESID_BF16 = 7,   // out_bf16[m][n] = bf16(out[m][n] + gate * (acc + bias))   (EPI_RESID_F32 on a bf16 residual
+                        // stream: fp32 math, one rounding -- the reference rounds twice, model.py:289)
 };
 
 struct GemmParams {
@@ -163,8 +165,8 @@ struct RopeNormParams {
 int rope_qknorm(const RopeNormParams& p, hipStream_t s);
 
 int patchify(const void* lat, bool in_bf16, bf16_t* out, int Bi, int C, int H, int W, int P, int dup, hipStream_t s);
-int fill_registers(float* x, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s);
-int add_pos_embed(float* x, const bf16_t* pos, int B, int T, int D, hipStream_t s);
+int fill_registers(void* x, bool x16, const bf16_t* reg, int B, int T, int R, int D, hipStream_t s);
+int add_pos_embed(void* x, bool x16, const bf16_t* pos, int B, int T, int D, hipStream_t s);
 int cfg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, int dup, float g, float dt,
               hipStream_t s);
 int cfg_euler_nchw(const float* u, const float* c, float* acc, long n, float g, float dt, int use_cfg,
@@ -175,8 +177,8 @@ int apg_update_nchw(const float* u, const float* c, float* acc, long n, float g,
                     hipStream_t s);
 int apg_sums_dev(const float* u, const float* c, long n, int phase, float* ws4, hipStream_t s);
 int rows_uniform(const void* x, int cols, const int* cu, int nseq, int* bad, hipStream_t s);
-int ctx_bcast_resid(float* x, const float* c, const float* gate, long gate_seg_stride, int rows_per_seg, long rows,
-                    int D, hipStream_t s);
+int ctx_bcast_resid(void* x, bool x16, const float* c, const float* gate, long gate_seg_stride, int rows_per_seg,
+                    long rows, int D, hipStream_t s);
 int apg_update_nchw_dev(const float* u, const float* c, float* acc, long n, float g, float thr, long n_total,
                         const float* ws4, float dt, hipStream_t s);
 int apg_euler(const float* out, float* acc, int Bi, int C, int H, int W, int P, float g, float thr, float dt,

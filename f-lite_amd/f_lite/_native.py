@@ -105,6 +105,9 @@ SIGNATURES = {
     "flite_dit_enable_fp8": (_i, [_vp, _vp, _i]),
     "flite_dit_set_fp8_bf16_blocks": (_i, [_vp, _vp, _i]),
     "flite_dit_set_fp8_gemm_classes": (_i, [_vp, _i]),
+    "flite_dit_set_fp8_block_classes": (_i, [_vp, _vp, _i]),
+    "flite_dit_set_residual_bf16": (_i, [_vp, _i]),
+    "flite_dit_residual_bf16": (_i, [_vp]),
     "flite_dit_weights_updated": (_i, [_vp, _vp]),
     "flite_vae_weights_updated": (_i, [_vp]),
     "flite_dit_set_sequence_parallel": (_i, [_vp, _i, _i, _vp, _vp]),
@@ -228,9 +231,13 @@ FP8_CLASSES = {"qkv": 1, "proj": 2, "cross_q": 4, "cross_proj": 8, "gate_up": 16
 
 
 def fp8_class_mask(classes) -> int:
-    """An int mask, or an iterable of FP8_CLASSES names ("all" = every class)."""
+    """An int mask, or an iterable of FP8_CLASSES names ("all" = every class). A bool is refused (True is not a
+    class set), and so is an empty name list: it would run every fp8 block in bf16 while the caller asked for fp8
+    (pass the int 0 to mean exactly that)."""
     if classes is None:
         return 63
+    if isinstance(classes, bool):
+        raise FliteError("fp8 GEMM classes: pass class names or an int mask, not a bool")
     if isinstance(classes, int):
         if not 0 <= classes <= 63:
             raise FliteError(f"fp8 GEMM class mask {classes} outside 0..63")
@@ -246,7 +253,33 @@ def fp8_class_mask(classes) -> int:
             m |= FP8_CLASSES[c]
         else:
             raise FliteError(f"unknown fp8 GEMM class {c!r} (one of {sorted(FP8_CLASSES)} or 'all')")
+    if m == 0:
+        raise FliteError("fp8 GEMM classes: empty class set (every fp8 block would run bf16); pass 0 to mean that")
     return m
+
+
+def fp8_block_masks(spec: str, depth: int, default=63) -> "list[int]":
+    """Per-block class masks from a policy string (bench.py --fp8-block-classes): ';'-separated "LO-HI:CLASSES" or
+    "I:CLASSES" items, CLASSES = '+'-separated FP8_CLASSES names, 'all', 'none' or an int mask; blocks no item
+    names get `default`. E.g. "0-3:none;4-7:gate_up+qkv" keeps blocks 0-3 bf16 and runs only gate/up and qkv
+    MXFP8 in blocks 4-7."""
+    masks = [int(default)] * depth
+    for item in (x.strip() for x in spec.split(";")):
+        if not item:
+            continue
+        rng, _, cls = item.partition(":")
+        if not cls:
+            raise FliteError(f"fp8 block policy item {item!r}: expected BLOCKS:CLASSES")
+        lo, _, hi = rng.partition("-")
+        lo, hi = int(lo), int(hi or lo)
+        if not 0 <= lo <= hi < depth:
+            raise FliteError(f"fp8 block policy item {item!r}: blocks outside 0..{depth - 1}")
+        cls = cls.strip()
+        m = 0 if cls == "none" else int(cls) if cls.isdigit() else fp8_class_mask(cls.split("+"))
+        if not 0 <= m <= 63:
+            raise FliteError(f"fp8 block policy item {item!r}: mask outside 0..63")
+        masks[lo:hi + 1] = [m] * (hi - lo + 1)
+    return masks
 
 
 def attn_workspace(device, batch, num_heads, max_q=0, max_k=0):
@@ -623,6 +656,24 @@ class DitEngine:
     def set_fp8_gemm_classes(self, mask: int = 63):
         """GEMM classes on MXFP8 in the fp8 blocks (include/flite.h flite_dit_set_fp8_gemm_classes)."""
         check(self.lib.flite_dit_set_fp8_gemm_classes(self.h, int(mask)), "flite_dit_set_fp8_gemm_classes")
+
+    def set_fp8_block_classes(self, masks=()):
+        """Per-block MXFP8 class masks (include/flite.h flite_dit_set_fp8_block_classes): one int per block, or
+        () to return to set_fp8_gemm_classes' single mask."""
+        masks = [int(m) for m in masks]
+        arr = (ctypes.c_int * max(len(masks), 1))(*masks)
+        check(self.lib.flite_dit_set_fp8_block_classes(self.h, arr, len(masks)), "flite_dit_set_fp8_block_classes")
+
+    def set_residual_bf16(self, on: bool = True):
+        """Residual-stream storage bf16 (on) or fp32 (include/flite.h flite_dit_set_residual_bf16)."""
+        check(self.lib.flite_dit_set_residual_bf16(self.h, int(bool(on))), "flite_dit_set_residual_bf16")
+
+    def residual_bf16(self) -> bool:
+        """True when the residual stream is held in bf16 (include/flite.h flite_dit_residual_bf16)."""
+        r = self.lib.flite_dit_residual_bf16(self.h)
+        if r < 0:
+            check(1, "flite_dit_residual_bf16")
+        return bool(r)
 
     def weights_updated(self, device=None):
         """The bound weights changed in place: remake the engine's derived copies (fp8: requantise)."""

@@ -111,13 +111,23 @@ def merge_lora_(model: torch.nn.Module, state_dict: Dict[str, torch.Tensor], sca
 _INT_OF = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}
 
 
+_FP_CHUNK = 1 << 24  # elements per fingerprint pass: bounds the int64 temporaries to ~0.7 GB
+
+
 def _fingerprint(W: torch.Tensor) -> Tuple[int, int, int]:
     """Position-weighted 64-bit sums of the tensor's raw bits (wrapping), on its own device: equal contents give equal
-    fingerprints wherever the tensor lives; a changed element changes them but for a 2^-64-scale accident."""
-    bits = W.detach().contiguous().reshape(-1).view(_INT_OF[W.element_size()]).to(torch.int64)
-    idx = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64)
-    mult = (idx * 2654435761 + 97) % 2147483629 + 1
-    return (int(bits.sum()), int((bits * mult).sum()), int((bits * bits * (idx % 8191 + 1)).sum()))
+    fingerprints wherever the tensor lives; a changed element changes them but for a 2^-64-scale accident. Hashed in
+    chunks of _FP_CHUNK elements (the sums wrap the same way chunked or whole)."""
+    flat = W.detach().contiguous().reshape(-1).view(_INT_OF[W.element_size()])
+    acc = torch.zeros(3, dtype=torch.int64, device=flat.device)
+    for c0 in range(0, flat.numel(), _FP_CHUNK):
+        bits = flat[c0:c0 + _FP_CHUNK].to(torch.int64)
+        idx = torch.arange(c0, c0 + bits.numel(), device=bits.device, dtype=torch.int64)
+        mult = (idx * 2654435761 + 97) % 2147483629 + 1
+        acc[0] += bits.sum()
+        acc[1] += (bits * mult).sum()
+        acc[2] += (bits * bits * (idx % 8191 + 1)).sum()
+    return tuple(int(v) for v in acc.tolist())
 
 
 def merged_state_dict(model: torch.nn.Module) -> Dict[str, torch.Tensor]:

@@ -165,6 +165,7 @@ class DiT(nn.Module):
         self._engine = None
         self._bound = None
         self._fp8 = False
+        self._resid16 = None  # residual-stream storage: None = the engine default, else bool (set_residual_dtype)
         self._wgen = 0
 
     # ------------------------------------------------------------------ construction helpers
@@ -319,6 +320,8 @@ class DiT(nn.Module):
         if self._engine is None:
             self._engine = _native.DitEngine(self._native_config())
             self._bound = None
+            if self._resid16 is not None:
+                self._engine.set_residual_bf16(self._resid16)
         if self._bound is None or self._bound[0] != ptrs:
             for n, p in params:
                 self._engine.bind(n, p.data)  # new storage: the engine requantises before its next run
@@ -327,17 +330,36 @@ class DiT(nn.Module):
         self._bound = (ptrs, vers)
         return self._engine
 
-    def enable_fp8(self, enabled: bool = True, bf16_blocks=(), gemm_classes=None):
+    def set_residual_dtype(self, dtype=torch.float32):
+        """Storage of the blocks' residual stream x (model.py:289,297,301): torch.float32 (the default, every update
+        fp32) or torch.bfloat16 (the reference's own storage; each update is still one fp32 fma, rounded once;
+        include/flite.h flite_dit_set_residual_bf16). No reference counterpart (the reference holds x in the model
+        dtype)."""
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("residual dtype must be torch.float32 or torch.bfloat16")
+        self._resid16 = dtype == torch.bfloat16
+        if self._engine is not None:
+            self._engine.set_residual_bf16(self._resid16)
+        return self
+
+    def enable_fp8(self, enabled: bool = True, bf16_blocks=(), gemm_classes=None, block_classes=None):
         """BASELINE.json configs[4]: run every block GEMM (qkv, proj, cross q / proj, SwiGLU gate-up, down) on
         MXFP8 weights and activations (OCP e4m3, E8M0 scale per 32 K elements) on the gfx950 block-scaled MFMA.
         The bf16 parameters stay the source of truth; the engine quantises them once. Precision policies (DESIGN §5
         prices each): `bf16_blocks`, block indices that keep their bf16 GEMMs (e.g. (0, depth - 1)); `gemm_classes`,
         the GEMM classes that run MXFP8 in the other blocks (names of _native.FP8_CLASSES, e.g. ("gate_up",), or an
-        int mask; None = all). No reference counterpart (the reference runs bf16 only)."""
+        int mask; None = all); `block_classes`, one class set per block (each as `gemm_classes`; 0 = that block bf16),
+        which overrides `gemm_classes` (include/flite.h flite_dit_set_fp8_block_classes). No reference counterpart
+        (the reference runs bf16 only)."""
         self._fp8 = bool(enabled)
         eng = self.engine()
         eng.set_fp8_bf16_blocks(bf16_blocks)
         eng.set_fp8_gemm_classes(_native.fp8_class_mask(gemm_classes))
+        if block_classes is not None and len(block_classes) != self.config.depth:
+            raise ValueError(f"block_classes: one class set per block ({self.config.depth}), got {len(block_classes)}")
+        eng.set_fp8_block_classes([] if block_classes is None else
+                                  [c if isinstance(c, int) and not isinstance(c, bool) else _native.fp8_class_mask(c)
+                                   for c in block_classes])
         eng.enable_fp8(self._fp8, self.device)
         return self
 

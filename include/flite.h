@@ -313,6 +313,23 @@ int flite_dit_set_fp8_bf16_blocks(flite_dit* dit, const int* blocks, int n);
 #define FLITE_FP8_ALL 63
 int flite_dit_set_fp8_gemm_classes(flite_dit* dit, int mask);
 /*
+ * fp8 precision policy per block (round 6): masks[i] = the FLITE_FP8_* classes block i runs on MXFP8 (0 = the
+ * whole block bf16), one mask per block (n_blocks = depth); n_blocks = 0 returns to the single mask of
+ * flite_dit_set_fp8_gemm_classes. flite_dit_set_fp8_bf16_blocks still forces its blocks to bf16. The classes are
+ * those of model.py:151-156,212 (attention) and :261-267 (SwiGLU MLP) per DiTBlock.
+ */
+int flite_dit_set_fp8_block_classes(flite_dit* dit, const int* masks, int n_blocks);
+/*
+ * Residual-stream storage (round 6): enable=1 keeps the DiTBlock residual x (model.py:289,297,301) in bf16, the
+ * reference's own storage type, instead of the default fp32. Every update stays one fp32 fma rounded once
+ * (the reference rounds gate*f and x + (.) separately, model.py:289); the norms read 2 B per element instead of 4
+ * and the gated-residual GEMM epilogues move 4 B instead of 8. Drops a cached graph; takes effect at the next
+ * forward / sample.
+ */
+int flite_dit_set_residual_bf16(flite_dit* dit, int enable);
+/* 1: the residual stream is bf16, 0: fp32 (the default unless FLITE_RESID_BF16=1 at engine creation), -1: error */
+int flite_dit_residual_bf16(flite_dit* dit);
+/*
  * The CONTENTS of bound weights changed in place (a load_state_dict copy, a LoRA merge, re-initialisation):
  * every engine-owned copy derived from them is remade -- in fp8 mode the MXFP8 weights are requantised on
  * `stream` now. The bf16 path reads the bound storage directly. The cross-attention K/V cached by

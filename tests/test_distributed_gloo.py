@@ -8,6 +8,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from _mp import pack, unpack  # tensors by value: a worker may exit before the parent reads its result
+
 
 def _free_port():
     s = socket.socket()
@@ -115,7 +117,7 @@ def _cfg_parallel_worker(rank, world, port, q):
         x += dt * (u + 6.0 * (c - u))
 
     acc = cfg_parallel_loop(lat.clone(), [t for t, _ in sched], [dt for _, dt in sched], forward_branch, update)
-    q.put((rank, acc))
+    q.put((rank, pack(acc)))
     dist.destroy_process_group()
 
 
@@ -138,7 +140,7 @@ def test_cfg_parallel_loop_matches_batched_oracle():
     procs = [ctx.Process(target=_cfg_parallel_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=180) for _ in range(2))
+    res = {r: unpack(v) for r, v in (q.get(timeout=180) for _ in range(2))}
     for p in procs:
         p.join(60)
     assert torch.equal(res[0], res[1])
@@ -203,7 +205,7 @@ def _dp_apg_worker(rank, world, port, q):
         apg_step(x, u, c, dt, 6.0, 0.03, n_total, sums, update, reduce=all_reduce_sum_)
 
     acc = data_parallel_loop(lat[mine].clone(), [dt for _, dt in sched], forward_pair, combine)
-    q.put((rank, gather_images(acc, lat.shape[0])))
+    q.put((rank, pack(gather_images(acc, lat.shape[0]))))
     dist.destroy_process_group()
 
 
@@ -228,7 +230,7 @@ def test_data_parallel_apg_matches_batched_oracle(world):
     procs = [ctx.Process(target=_dp_apg_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(world))
+    res = {r: unpack(v) for r, v in (q.get(timeout=240) for _ in range(world))}
     for p in procs:
         p.join(60)
     for r in range(1, world):

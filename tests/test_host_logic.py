@@ -293,3 +293,22 @@ def test_apg_step_scalar_algebra_matches_reference():
     orth = dd - (dy * dd).sum() / (dy * dy).sum() * dy
     want = acc + 0.1 * (dy + 5.0 * orth * min(1, 0.03 / orth.std()))
     torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+
+
+def test_fp8_policy_parsing():
+    """_native.fp8_class_mask refuses a bool and an empty class set (`--fp8-classes ''` silently ran
+    bf16); fp8_block_masks expands the per-block policy strings of bench.py --fp8-block-classes
+    (include/flite.h flite_dit_set_fp8_block_classes)."""
+    from f_lite import _native as nat
+
+    assert nat.fp8_class_mask(None) == 63 and nat.fp8_class_mask("all") == 63 and nat.fp8_class_mask(0) == 0
+    assert nat.fp8_class_mask(["gate_up", "qkv"]) == 17
+    for bad in (True, "", [], "nope"):
+        with pytest.raises(nat.FliteError):
+            nat.fp8_class_mask(bad)
+    m = nat.fp8_block_masks("0-3:none;4-7:gate_up+qkv;39:32", 40, default=63)
+    assert m[:4] == [0] * 4 and m[4:8] == [17] * 4 and m[8:39] == [63] * 31 and m[39] == 32
+    assert nat.fp8_block_masks("", 3, default=5) == [5, 5, 5]
+    for bad in ("0-40:all", "3", "2-1:all", "0:64"):
+        with pytest.raises(nat.FliteError):
+            nat.fp8_block_masks(bad, 40)
