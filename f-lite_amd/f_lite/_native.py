@@ -19,6 +19,7 @@ EPI_STORE_F32 = 1
 EPI_RESID_F32 = 2
 EPI_SWIGLU_BF16 = 3
 EPI_GEGLU_BF16 = 6
+EPI_RESID_BF16 = 7
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
@@ -120,6 +121,7 @@ SIGNATURES = {
 
 EPI8_STORE_BF16 = 0
 EPI8_RESID_F32 = 2
+EPI8_RESID_BF16 = 7
 EPI8_SWIGLU_FP8 = 4
 
 PROBE_GEMM_GATEUP = 0

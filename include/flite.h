@@ -34,6 +34,7 @@ int flite_version(void);
 #define FLITE_EPI_RESID_F32 2   /* out_f32[m][n]  += gate[m/rows_per_seg][n] * (A.W^T + bias)      */
 #define FLITE_EPI_SWIGLU_BF16 3 /* out_bf16[m][f]  = silu(A.Wg^T)[f] * (A.Wu^T)[f], N = 2F          */
 #define FLITE_EPI_GEGLU_BF16 6  /* out_bf16[m][f]  = gelu_tanh(A.Wg^T)[f] * (A.Wu^T)[f], N = 2F (T5)  */
+#define FLITE_EPI_RESID_BF16 7  /* out_bf16[m][n]  = bf16(out + gate * (A.W^T + bias)), fp32 math      */
 
 /*
  * bf16 GEMM with fused epilogue: C[M,N] = A[M,K] . W[N,K]^T  (W in nn.Linear [out,in] layout).
@@ -132,6 +133,7 @@ int flite_rope_qknorm(void* stream, void* x, long ldx, long rows, int heads, int
  * ------------------------------------------------------------------------------------------- */
 #define FLITE_EPI8_STORE_BF16 0  /* out_bf16[m][n]  = A.W^T + bias                                   */
 #define FLITE_EPI8_RESID_F32 2   /* out_f32[m][n]  += gate[m/rows_per_seg][n] * (A.W^T + bias)       */
+#define FLITE_EPI8_RESID_BF16 7  /* out_bf16[m][n]  = bf16(out + gate * (A.W^T + bias)), fp32 math     */
 #define FLITE_EPI8_SWIGLU_FP8 4  /* out_fp8[m][f]   = MX(silu(A.Wg^T) * (A.Wu^T)), W = gate|up interleaved in
                                     16-row sub-tiles (flite_quant_fp8_gateup), N = 2F; scales to out_scales */
 

@@ -347,3 +347,87 @@ def test_fp8_first_blocks_bf16_1024_cfg1_vs_reference(gold4, m7b, m10b, name):
     print(f"fp8 {name} 1024^2 30-step CFG-1 final latents vs reference fp32: " +
           ", ".join(f"{k} {v:.2f} dB" for k, v in res.items()))
     assert res["bf16 blocks 0-7"] >= 40.0
+
+
+# ---- the reference's DEFAULT configuration pinned end to end (tests/golden/make_golden_full5.py) --
+@pytest.fixture(scope="module")
+def gold5():
+    from safetensors.torch import load_file
+
+    f = GOLD / "golden_full5.safetensors"
+    if not f.exists():
+        pytest.skip("golden_full5.safetensors not generated")
+    return load_file(str(f)), json.loads((GOLD / "golden_full5_meta.json").read_text())
+
+
+def _uint8_psnr(img, ref):
+    return 10 * math.log10(255.0 ** 2 / max((img.double() - ref.double()).pow(2).mean().item(), 1e-12))
+
+
+@pytest.mark.parametrize("g", [1.0, 6.0])
+def test_10b_1344x896_30_steps_vs_reference(gold5, m10b, g):
+    """generate.py:19-22's defaults end to end against the reference itself: 10B (model_v2 layout), 1344x896 (T = 4720:
+    the non-square 56 x 84 RoPE grid of model.py:334-400, alpha = 4.2866 from pipeline.py:240-242, 112-row attention
+    tails and the 256-row attention route), 30 steps, the hipGraph loop the bench times, then generate.py:77-78's tiled
+    VAE decode (2 x 2 overlapping tiles) to uint8. Final latents vs the reference's fp32 trajectory: >= 40 dB at CFG 1
+     and at least the reference's own bf16 run; at CFG 6, at least the reference's own bf16 run. The uint8
+    image vs oracle/vae_ref.py's tiled decode of the reference latents: >= 40 dB at CFG 1, at CFG 6 at least the
+    reference's bf16 image."""
+    from f_lite.vae import AutoencoderKL
+
+    gd, meta = gold5
+    key = f"10b.1344x896.s30.g{g:g}"
+    if f"{key}.f32.final" not in gd:
+        pytest.skip(f"{key}.f32.final not generated yet (tests/golden/make_golden_full5.py)")
+    floor = meta.get(f"{key}.bf16_vs_f32_psnr")
+    if g != 1.0 and floor is None:
+        pytest.skip(f"{key}.bf16 (the CFG-6 floor) not generated yet (tests/golden/make_golden_full5.py)")
+    assert abs(meta["alpha"] - 4.2866) < 1e-4
+    pipe = FLitePipeline(m10b, vae=AutoencoderKL.random(seed=0))
+    pipe.enable_vae_tiling()
+    kw = dict(prompt_embeds=hashed(meta, "ctx"), latents=hashed(meta, "latents"), height=896, width=1344,
+              num_inference_steps=30, guidance_scale=g, use_graph=True)
+    lat = pipe(**kw, output_type="latent").images.float()
+    p = psnr(lat / SCALING + SHIFT, gd[f"{key}.f32.final"])
+    print(f"10b 1344x896 30-step CFG-{g:g} final latents: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
+          f"{'n/a' if floor is None else f'{floor:.2f} dB'})")
+    if g == 1.0:
+        assert p >= 40.0
+    if floor is not None:
+        assert p >= floor
+    ref = gd.get(f"{key}.f32.image")
+    if ref is None:
+        pytest.skip(f"{key}.f32.image not decoded yet")
+    img = pipe(**kw, output_type="uint8").images.cpu()
+    assert img.shape == ref.shape == (1, 896, 1344, 3)
+    pi = _uint8_psnr(img, ref)
+    ifloor = meta.get(f"{key}.image_bf16_vs_f32_psnr")
+    print(f"  uint8 image (HIP loop + HIP tiled VAE) vs oracle tiled VAE on the reference latents: {pi:.2f} dB "
+          f"(the reference's own bf16 run: {'n/a' if ifloor is None else f'{ifloor:.2f} dB'})")
+    if g == 1.0:
+        assert pi >= 40.0
+    if ifloor is not None:
+        assert pi >= ifloor
+
+
+def test_fp8_first_blocks_bf16_1344x896_cfg1_vs_reference(gold5, m10b):
+    """BASELINE configs[4]'s MXFP8 path at its own size (1344x896) against the reference's fp32 trajectory at CFG 1:
+    the quality policy (blocks 0-7 bf16, MXFP8 elsewhere) meets the SURVEY §8d bar of 40 dB; the all-fp8 default is
+    printed beside it."""
+    gd, meta = gold5
+    key = "10b.1344x896.s30.g1"
+    if f"{key}.f32.final" not in gd:
+        pytest.skip(f"{key}.f32.final not generated yet")
+    kw = dict(prompt_embeds=hashed(meta, "ctx"), latents=hashed(meta, "latents"), height=896, width=1344,
+              num_inference_steps=30, guidance_scale=1.0, output_type="latent")
+    res = {}
+    try:
+        for label, blocks in (("all fp8", []), ("bf16 blocks 0-7", list(range(8)))):
+            m10b.enable_fp8(True, bf16_blocks=blocks)
+            lat = FLitePipeline(m10b)(**kw).images.float()
+            res[label] = psnr(lat / SCALING + SHIFT, gd[f"{key}.f32.final"])
+    finally:
+        m10b.enable_fp8(False, bf16_blocks=[])
+    print("fp8 10b 1344x896 30-step CFG-1 final latents vs reference fp32: " +
+          ", ".join(f"{k} {v:.2f} dB" for k, v in res.items()))
+    assert res["bf16 blocks 0-7"] >= 40.0

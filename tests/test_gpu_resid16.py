@@ -1,0 +1,182 @@
+"""GPU: the bf16 residual stream (include/flite.h flite_dit_set_residual_bf16, DiT.set_residual_dtype; VERDICT r05
+next 2) against the fp32 oracle and against the fp32-residual path.
+
+The reference holds the DiTBlock residual x in the model dtype and rounds twice per update (`x + gate * f(...)`,
+model.py:289,297,301); the bf16 residual stream keeps that storage but each update is ONE fp32 fma rounded once
+(EPI_RESID_BF16 / EPI8_RESID_BF16 epilogues, the bf16 rows of rmsnorm_mod_row_kernel's deferred broadcast update).
+Kernel bars: the gated-residual epilogues equal bf16(x + gate * (A.W^T + bias)) of an fp32 reference to within the
+accumulation-order difference (rel <= 4e-3, one bf16 ulp); engine bars: the SURVEY §8d forward bar (>= 40 dB vs the
+fp32 oracle), graph == eager, and the 30-step metric trajectory against the reference itself (tests/golden
+golden_full4: >= 40 dB at CFG 1, at least the reference's own bf16 run at CFG 6).
+"""
+import json
+import math
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no ROCm device", allow_module_level=True)
+
+from f_lite import DiT, FLitePipeline  # noqa: E402
+from f_lite import _native as nat  # noqa: E402
+from f_lite.model import PRESETS  # noqa: E402
+from oracle import flite_ref as R  # noqa: E402
+
+DEV = "cuda"
+GOLD = Path(__file__).resolve().parent / "golden"
+SCALING, SHIFT = 0.3611, 0.1159
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / b.norm()).item()
+
+
+def psnr(a, ref):
+    a, ref = a.double().cpu(), ref.double().cpu()
+    mse = (a - ref).pow(2).mean().item()
+    return float("inf") if mse == 0 else 10 * math.log10(ref.abs().max().item() ** 2 / mse)
+
+
+# segments of 300 rows (per-row and two-segment gate paths), 224-row tiles (M = 8224, N = 3072), stream-K (K = 12288)
+@pytest.mark.parametrize("M,N,K,T", [(1000, 768, 256, 300), (8224, 3072, 128, 4112), (8224, 3072, 12288, 4112)])
+def test_gemm_gated_residual_bf16(M, N, K, T):
+    g = torch.Generator().manual_seed(M + K)
+    a = torch.randn(M, K, generator=g).bfloat16().to(DEV)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).bfloat16().to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).bfloat16().to(DEV)
+    nseg = (M + T - 1) // T
+    gate = torch.randn(nseg, N, generator=g).to(DEV)
+    x0 = (torch.randn(M, N, generator=g) * 4).bfloat16().to(DEV)
+    y = a.float() @ w.float().t() + b.float()
+    seg = torch.arange(M, device=DEV) // T
+    ref = (x0.float() + y * gate[seg]).bfloat16()
+    x = x0.clone()
+    nat.gemm(a, w, b, out=x, epilogue=nat.EPI_RESID_BF16, gate=gate, gate_seg_stride=N, rows_per_seg=T,
+             workspace=nat.gemm_workspace(DEV) if K >= 4096 else None)
+    assert x.dtype == torch.bfloat16
+    assert rel(x, ref) < 4e-3
+    # most elements round to the same bf16 value (the only difference is the fp32 accumulation order)
+    assert (x != ref).float().mean().item() < 0.05
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 512), (8224, 3072, 3072), (8224, 3072, 12288)])
+def test_gemm_fp8_gated_residual_bf16(M, N, K):
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).bfloat16().to(DEV)
+    w = (torch.randn(N, K, generator=g) * 0.02).bfloat16().to(DEV)
+    a8, asc = nat.quant_fp8_rows(a)
+    w8, wsc = nat.quant_fp8_rows(w)
+    gate = torch.randn(1, N, generator=g).to(DEV)
+    x0 = (torch.randn(M, N, generator=g) * 4).bfloat16().to(DEV)
+    x32 = x0.float()
+    nat.gemm_fp8(a8, asc, w8, wsc, out=x32, epilogue=nat.EPI8_RESID_F32, gate=gate, gate_seg_stride=0,
+                 rows_per_seg=M, workspace=nat.gemm_workspace(DEV))
+    x = x0.clone()
+    nat.gemm_fp8(a8, asc, w8, wsc, out=x, epilogue=nat.EPI8_RESID_BF16, gate=gate, gate_seg_stride=0,
+                 rows_per_seg=M, workspace=nat.gemm_workspace(DEV))
+    # the same fp32 value (same kernel, same accumulation), rounded once at the store
+    assert torch.equal(x, x32.bfloat16())
+
+
+@pytest.fixture(scope="module")
+def tiny16():
+    return DiT.random(seed=0, **PRESETS["tiny"]).set_residual_dtype(torch.bfloat16)
+
+
+def test_residual_dtype_switch_round_trips(tiny16):
+    eng = tiny16.engine()
+    assert eng.residual_bf16()
+    tiny16.set_residual_dtype(torch.float32)
+    assert not eng.residual_bf16()
+    tiny16.set_residual_dtype(torch.bfloat16)
+    assert eng.residual_bf16()
+    with pytest.raises(ValueError):
+        tiny16.set_residual_dtype(torch.float16)
+
+
+def test_forward_bf16_residual_vs_oracle(golden, tiny16):
+    """SURVEY §8d P1/P2 bar (>= 40 dB vs the fp32 oracle) with the residual stream in bf16, v1 and v2 layouts; the
+    fp32-residual forward is printed beside it."""
+    x, ctx, t = golden["in.x"].bfloat16(), golden["in.ctx"].bfloat16(), golden["in.t"]
+    ref = R.RefDiT.random(R.PRESETS["tiny"], dtype=torch.float32)(x.float(), ctx.float(), None, t)
+    out16 = tiny16(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32)
+    m32 = DiT.random(seed=0, **PRESETS["tiny"]).set_residual_dtype(torch.float32)
+    out32 = m32(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32)
+    p16, p32 = psnr(out16, ref), psnr(out32, ref)
+    print(f"tiny forward vs fp32 oracle: bf16 residual {p16:.2f} dB, fp32 residual {p32:.2f} dB")
+    assert p16 >= 40.0
+    v2 = DiT.random(seed=0, **PRESETS["tiny_v2"]).set_residual_dtype(torch.bfloat16)
+    ref2 = R.RefDiT.random(R.PRESETS["tiny_v2"], dtype=torch.float32)(x.float(), ctx.float(), None, t)
+    p2 = psnr(v2(x.to(DEV), ctx.to(DEV), None, t.to(DEV), output_dtype=torch.float32), ref2)
+    print(f"tiny_v2 forward vs fp32 oracle: bf16 residual {p2:.2f} dB")
+    assert p2 >= 40.0
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_bf16_residual_loop_graph_equals_eager(golden, fp8):
+    """The 4-step CFG-6 loop with the zero negative prompt (uniform-context collapse, block-0 dedup) and a random
+    negative context: hipGraph replay == eager bit for bit, bf16 and MXFP8 blocks; close to the fp32-residual loop."""
+    m = DiT.random(seed=0, **PRESETS["10b"] | {"depth": 2}).set_residual_dtype(torch.bfloat16)
+    if fp8:
+        m.enable_fp8(True)
+    lat = torch.empty(1, 16, 32, 32, device=DEV, dtype=torch.bfloat16)
+    nat.init_param_(lat, "synthetic.latents.0", seed=2, std=1.0)
+    pos = torch.empty(1, 64, 4096, device=DEV, dtype=torch.bfloat16)
+    nat.init_param_(pos, "synthetic.t5_context", seed=1, std=1.0)
+    neg = torch.empty_like(pos)
+    nat.init_param_(neg, "synthetic.t5_negative_context", seed=3, std=1.0)
+    pipe = FLitePipeline(m)
+    outs = {}
+    for name, negative in (("zero", None), ("random", neg)):
+        kw = dict(prompt_embeds=pos, negative_prompt_embeds=negative, latents=lat, height=256, width=256,
+                  num_inference_steps=4, guidance_scale=6.0, output_type="latent")
+        a = pipe(**kw, use_graph=True).images.float()
+        b = pipe(**kw, use_graph=False).images.float()
+        assert torch.isfinite(a).all() and torch.equal(a, b)
+        outs[name] = a
+    m.set_residual_dtype(torch.float32)
+    for name, negative in (("zero", None), ("random", neg)):
+        c = pipe(prompt_embeds=pos, negative_prompt_embeds=negative, latents=lat, height=256, width=256,
+                 num_inference_steps=4, guidance_scale=6.0, output_type="latent").images.float()
+        p = psnr(outs[name], c)
+        print(f"{'fp8' if fp8 else 'bf16'} blocks, {name} negative: bf16 vs fp32 residual after 4 CFG-6 steps "
+              f"{p:.2f} dB")
+        assert p >= (25.0 if fp8 else 30.0)
+
+
+@pytest.fixture(scope="module")
+def gold4():
+    from safetensors.torch import load_file
+
+    f = GOLD / "golden_full4.safetensors"
+    if not f.exists():
+        pytest.skip("golden_full4.safetensors not generated")
+    return load_file(str(f)), json.loads((GOLD / "golden_full4_meta.json").read_text())
+
+
+@pytest.mark.parametrize("g", [1.0, 6.0])
+def test_10b_1024_30_steps_bf16_residual_vs_reference(gold4, g):
+    """The metric workload (10B, 1024^2, 30 steps, hipGraph loop) with the bf16 residual stream against the reference's
+    fp32 trajectory: >= 40 dB at CFG 1 and at least the reference's own bf16 run at both guidances."""
+    gd, meta = gold4
+    key = f"10b.1024.s30.g{g:g}"
+    m = DiT.random(seed=0, device=DEV, **PRESETS["10b"]).set_residual_dtype(torch.bfloat16)
+
+    def hashed(k):
+        name, shape = meta["inputs"][k]
+        return nat.init_param_(torch.empty(*shape, device=DEV, dtype=torch.bfloat16), name, seed=0, std=1.0)
+
+    lat = FLitePipeline(m)(prompt_embeds=hashed("ctx"), latents=hashed("latents_1024"), height=1024, width=1024,
+                           num_inference_steps=30, guidance_scale=g, output_type="latent").images.float()
+    p = psnr(lat / SCALING + SHIFT, gd[f"{key}.f32.final"])
+    floor = meta[f"{key}.bf16_vs_f32_psnr"]
+    print(f"10b 1024^2 30-step CFG-{g:g}, bf16 residual: {p:.2f} dB vs reference fp32 (reference's own bf16 run: "
+          f"{floor:.2f} dB)")
+    assert p >= floor
+    if g == 1.0:
+        assert p >= 40.0
