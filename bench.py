@@ -314,8 +314,8 @@ def main():
                     help="with --fp8: per-block class policy, _native.fp8_block_masks syntax (e.g. "
                          "'0-3:none;4-7:gate_up+qkv'); overrides --fp8-classes for the blocks it names")
     ap.add_argument("--residual", default=None, choices=["fp32", "bf16"],
-                    help="residual-stream storage (DiT.set_residual_dtype); default: the engine's (fp32 unless "
-                         "FLITE_RESID_BF16=1)")
+                    help="residual-stream storage (DiT.set_residual_dtype); default: the engine's (bf16 unless "
+                         "FLITE_RESID_BF16=0)")
     ap.add_argument("--probe", default="gateup", choices=["gateup", "attn", "down", "qkv", "step", "none"])
     ap.add_argument("--mode", default="replica", choices=["replica", "cfg-parallel", "sp", "sp-ring"],
                     help="replica: image i on GPU i mod N (the metric line); cfg-parallel: the two CFG branches of an "

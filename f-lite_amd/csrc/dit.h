@@ -140,10 +140,11 @@ class DitEngine {
   int collapse_fp8(hipStream_t s);
   int uni_fp8() const;
   // workspace
-  // residual stream [M, D]: fp32, or bf16 with x16_ (flite_dit_set_residual_bf16; the reference's own storage type,
-  // model.py:289). Every writer is an fp32 fma with one rounding; the buffer is sized for fp32 either way.
+  // residual stream [M, D]: bf16 (x16_, the default since round 6: the reference's own storage type, model.py:289) or
+  // fp32 (flite_dit_set_residual_bf16(dit, 0)). Every writer is an fp32 fma with one rounding; the buffer is sized
+  // for fp32 either way.
   void* x_ = nullptr;
-  bool x16_ = false;
+  bool x16_ = true;
   size_t xbytes() const { return x16_ ? 2 : 4; }
   void* xrow(long r) const { return (char*)x_ + r * (long)D * (long)xbytes(); }
   int epi_resid() const { return x16_ ? EPI_RESID_BF16 : EPI_RESID_F32; }

@@ -330,11 +330,11 @@ class DiT(nn.Module):
         self._bound = (ptrs, vers)
         return self._engine
 
-    def set_residual_dtype(self, dtype=torch.float32):
-        """Storage of the blocks' residual stream x (model.py:289,297,301): torch.float32 (the default, every update
-        fp32) or torch.bfloat16 (the reference's own storage; each update is still one fp32 fma, rounded once;
-        include/flite.h flite_dit_set_residual_bf16). No reference counterpart (the reference holds x in the model
-        dtype)."""
+    def set_residual_dtype(self, dtype=torch.bfloat16):
+        """Storage of the blocks' residual stream x (model.py:289,297,301): torch.bfloat16 (the default since round 6:
+        the reference's own storage, each update still one fp32 fma rounded once) or torch.float32 (every update and
+        the stream in fp32: 1.5-3 dB closer to the reference's fp32 run, 1.5 % slower). include/flite.h
+        flite_dit_set_residual_bf16."""
         if dtype not in (torch.float32, torch.bfloat16):
             raise ValueError("residual dtype must be torch.float32 or torch.bfloat16")
         self._resid16 = dtype == torch.bfloat16

@@ -322,14 +322,14 @@ int flite_dit_set_fp8_gemm_classes(flite_dit* dit, int mask);
  */
 int flite_dit_set_fp8_block_classes(flite_dit* dit, const int* masks, int n_blocks);
 /*
- * Residual-stream storage (round 6): enable=1 keeps the DiTBlock residual x (model.py:289,297,301) in bf16, the
- * reference's own storage type, instead of the default fp32. Every update stays one fp32 fma rounded once
- * (the reference rounds gate*f and x + (.) separately, model.py:289); the norms read 2 B per element instead of 4
- * and the gated-residual GEMM epilogues move 4 B instead of 8. Drops a cached graph; takes effect at the next
- * forward / sample.
+ * Residual-stream storage (round 6): enable=1 (the default) keeps the DiTBlock residual x (model.py:289,297,301) in
+ * bf16, the reference's own storage type; enable=0 keeps it in fp32. Every update stays one fp32 fma rounded once
+ * (the reference rounds gate*f and x + (.) separately, model.py:289); in bf16 the norms read 2 B per element
+ * instead of 4 and the gated-residual GEMM epilogues move 4 B instead of 8 (+1.55 % images/s at the metric
+ * workload). Drops a cached graph; takes effect at the next forward / sample.
  */
 int flite_dit_set_residual_bf16(flite_dit* dit, int enable);
-/* 1: the residual stream is bf16, 0: fp32 (the default unless FLITE_RESID_BF16=1 at engine creation), -1: error */
+/* 1: the residual stream is bf16 (the default unless FLITE_RESID_BF16=0 at engine creation), 0: fp32, -1: error */
 int flite_dit_residual_bf16(flite_dit* dit);
 /*
  * The CONTENTS of bound weights changed in place (a load_state_dict copy, a LoRA merge, re-initialisation):

@@ -327,6 +327,7 @@ for name, cfg, hw, fp8 in (("tiny", dict(PRESETS["tiny"]), 128, None),
     out[f"{{name}}.fwd"] = m(torch.cat([x[:1], x[:1]]), torch.cat([negs["zero"][:1], pos[:1]]), None, t,
                              output_dtype=torch.float32).cpu()
     out[f"{{name}}.lat"], out[f"{{name}}.pos"] = lat.float().cpu(), pos.float().cpu()
+    out["resid16"] = torch.tensor(int(m.engine().residual_bf16()))
 torch.save(out, sys.argv[1])
 """
 
@@ -342,7 +343,9 @@ def test_uniform_context_collapse_matches_full_computation(tmp_path):
     negative context is not collapsed (bit-identical). MXFP8 (all blocks, and block 0 bf16 + block 1 fp8): the
     collapse quantises V where the full path quantises the attention output (V to within a bf16 ulp), which moves an
     occasional e4m3 rounding: >= 30 dB between the two, and against the bf16 full computation the collapse is at least
-    as close as the full fp8 path (-0.5 dB slack)."""
+    as close as the full fp8 path (-0.5 dB slack). With the bf16 residual stream (flite_dit_set_residual_bf16) that
+    ulp can flip a rounding of the stored residual, which the later blocks carry: the single forward's bar is then
+    55 dB instead of 60 (measured 59.35 dB, 10b_d2)."""
     import dataclasses
     import os
     import subprocess
@@ -377,7 +380,7 @@ def test_uniform_context_collapse_matches_full_computation(tmp_path):
                 assert pc >= pf - 0.5
         p = psnr(col[f"{name}.fwd"], full[f"{name}.fwd"])
         print(f"  forward with [zero, prompt] contexts: {p:.2f} dB")
-        assert p >= (35.0 if fp8 else 60.0)
+        assert p >= (35.0 if fp8 else 55.0 if int(col["resid16"]) else 60.0)
     for name, cfg, hw in (("tiny", R.PRESETS["tiny"], 128), ("10b_d2", dataclasses.replace(R.PRESETS["10b"], depth=2),
                                                              256)):
         ref = R.sample(R.RefDiT.random(cfg, dtype=torch.float32), col[f"{name}.lat"], col[f"{name}.pos"],
