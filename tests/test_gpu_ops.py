@@ -271,11 +271,13 @@ def test_attention_spike_rescale():
     assert rel(out, ref) < 1e-2
 
 
-# 3072: the one-workgroup-per-row kernel of the DiT width; 602 rows: a partial last group of the 4-row kernel
+# 3072: the one-workgroup-per-row kernel of the DiT width (bf16 rows: two per workgroup, rmsnorm_mod_row2_kernel);
+# 602 rows: a partial last group of the 4-row kernel; 603 rows of 251: a lone last row and row pairs that straddle a
+# modulation segment
+@pytest.mark.parametrize("rows,T", [(602, 250), (603, 251)])
 @pytest.mark.parametrize("D", [512, 3072])
 @pytest.mark.parametrize("in_bf16", [False, True])
-def test_rmsnorm_modulate(in_bf16, D):
-    rows, T = 602, 250
+def test_rmsnorm_modulate(in_bf16, D, rows, T):
     x = torch.randn(rows, D, device=DEV) * 3
     if in_bf16:
         x = x.bfloat16()
