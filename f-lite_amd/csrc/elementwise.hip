@@ -231,134 +231,6 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
   }
 }
 
-// The bf16 residual stream (round 6) at D = 3072: TWO rows per 256-thread workgroup. One bf16 row is 6 KB, half an
-// fp32 row, so one row per workgroup left too few bytes in flight per CU to cover the HBM latency (26.7 us for
-// 100 MB where the fp32 kernel moved 151 MB in 29 us, profiles/r06d); with two rows the loads of both are issued
-// before either reduction, and the weight / scale / shift rows (30 KB from L2) serve both rows when they share a
-// modulation segment. Thread t holds elements q*1024 + 4t .. +3 of each row, as the one-row kernel, and computes
-// the same per-element fp32 expression; BC / PF as there.
-template <bool OUT8, bool PF, bool BC>
-__global__ __launch_bounds__(256) void rmsnorm_mod_row2_kernel(NormModParams p) {
-  constexpr int NQ = 3;
-  __shared__ float part[2][4];
-  const int t = threadIdx.x;
-  const long m0 = 2L * blockIdx.x;
-  const bool two = m0 + 1 < p.rows;  // uniform over the workgroup
-  float v[2][4 * NQ];
-  long seg[2], in_row[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const long m = two ? m0 + r : m0;  // a lone last row is loaded twice and stored once
-    seg[r] = p.in_seg > 0 ? m / p.in_seg : 0;
-    in_row[r] = p.in_seg > 0 ? seg[r] * p.in_stride + p.in_off + (m % p.in_seg) : m;
-  }
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const bf16_t* xr = (const bf16_t*)p.x + in_row[r] * p.ldx;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const u32x2 w = *(const u32x2*)(xr + q * 1024 + t * 4);
-      v[r][4 * q + 0] = __uint_as_float(w.x << 16);
-      v[r][4 * q + 1] = __uint_as_float(w.x & 0xffff0000u);
-      v[r][4 * q + 2] = __uint_as_float(w.y << 16);
-      v[r][4 * q + 3] = __uint_as_float(w.y & 0xffff0000u);
-    }
-  }
-  if constexpr (BC) {  // rmsnorm_mod_row_kernel's bf16 deferred broadcast update, per row
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const long m = m0 + r;
-      if ((r == 0 || two) && m < p.bc_rows) {
-        const long bs = m / p.bc_rows_per_seg;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const int n = q * 1024 + t * 4;
-          const f32x4 cv = *(const f32x4*)(p.bc_c + bs * (long)(1024 * NQ) + n);
-          const f32x4 gv = *(const f32x4*)(p.bc_gate + bs * p.bc_gate_stride + n);
-          float nv[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) nv[j] = __builtin_fmaf(cv[j], gv[j], v[r][4 * q + j]);
-          const u32x2 st = {pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3])};
-          *(u32x2*)((bf16_t*)p.x + in_row[r] * p.ldx + n) = st;
-          v[r][4 * q + 0] = __uint_as_float(st.x << 16);
-          v[r][4 * q + 1] = __uint_as_float(st.x & 0xffff0000u);
-          v[r][4 * q + 2] = __uint_as_float(st.y << 16);
-          v[r][4 * q + 3] = __uint_as_float(st.y & 0xffff0000u);
-        }
-      }
-    }
-  }
-  const bool same = seg[0] == seg[1];  // uniform
-  float wgt[NQ][4];
-  f32x4 sc[2][NQ], sh[2][NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int n = q * 1024 + t * 4;
-    wgt[q][0] = wgt[q][1] = wgt[q][2] = wgt[q][3] = 1.f;
-    if (p.w) {
-      const u32x2 ww = *(const u32x2*)(p.w + n);
-      wgt[q][0] = __uint_as_float(ww.x << 16);
-      wgt[q][1] = __uint_as_float(ww.x & 0xffff0000u);
-      wgt[q][2] = __uint_as_float(ww.y << 16);
-      wgt[q][3] = __uint_as_float(ww.y & 0xffff0000u);
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      if (r == 1 && same) {
-        sc[1][q] = sc[0][q];
-        sh[1][q] = sh[0][q];
-        continue;
-      }
-      sc[r][q] = p.scale ? *(const f32x4*)(p.scale + seg[r] * p.mod_seg_stride + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      sh[r][q] = p.shift ? *(const f32x4*)(p.shift + seg[r] * p.mod_seg_stride + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  float ss[2] = {0.f, 0.f};
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-#pragma unroll
-    for (int i = 0; i < 4 * NQ; ++i) ss[r] += v[r][i] * v[r][i];
-    ss[r] = wave_sum(ss[r]);
-  }
-  if ((t & 63) == 0) {
-    part[0][t >> 6] = ss[0];
-    part[1][t >> 6] = ss[1];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    if (r == 1 && !two) break;
-    const float tot = part[r][0] + part[r][1] + part[r][2] + part[r][3];
-    const float rs = rsqrtf(tot / (float)(1024 * NQ) + p.eps);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int n = q * 1024 + t * 4;
-      float o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = v[r][4 * q + j] * rs * wgt[q][j] * (1.f + sc[r][q][j]) + sh[r][q][j];
-      norm_store4<OUT8>(p, m0 + r, n, o);
-    }
-  }
-  if constexpr (PF) {  // rmsnorm_mod_row_kernel's read-ahead, by workgroup
-    constexpr int NPF = 6;
-    unsigned pf_acc = 0;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      if (p.pf[r] == nullptr) continue;
-      const long pieces = p.pf_bytes[r] >> 12;
-      u32x4 pv[NPF];
-#pragma unroll
-      for (int k = 0; k < NPF; ++k) {
-        const long i = (long)blockIdx.x + (long)k * gridDim.x;
-        pv[k] = i < pieces ? ((const u32x4*)((const char*)p.pf[r] + (i << 12)))[t] : u32x4{0u, 0u, 0u, 0u};
-      }
-#pragma unroll
-      for (int k = 0; k < NPF; ++k) pf_acc ^= pv[k].x ^ pv[k].w;
-    }
-    if (p.pf_bytes[0] < 0 && pf_acc == 0x9e3779b9u) part[0][0] = 0.f;
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // RoPE (2-D, rotate-half pairs (j, j+128), rotation by -theta) + per-head RMSNorm (no weight), in place
 // on bf16 heads of 256. Reference: apply_rotary_emb (model.py:403-414) then QKNorm (model.py:115-126,180,197).
@@ -799,12 +671,6 @@ int grid_for(long total, int per_block = 256) {
   return (int)g;
 }
 
-// bf16 rows at D = 3072 take rmsnorm_mod_row2_kernel (FLITE_NORM_ROW1=1: the one-row kernel, an A/B switch)
-bool norm_row2() {
-  static const bool on = getenv("FLITE_NORM_ROW1") == nullptr;
-  return on;
-}
-
 }  // namespace
 
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
@@ -815,16 +681,7 @@ int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   if (p.y8 != nullptr) {  // MXFP8 output (fp8 DiT path): fp32 or bf16 residual rows
     FLITE_REQUIRE(p.ysc != nullptr && p.ysc_rows_pad >= mx_rows_pad(p.rows) && p.D % 128 == 0 && p.ldy % 16 == 0,
                   "rmsnorm(fp8 out): scales for the padded rows, D % 128, 16-B row stride");
-    if (p.D == 3072 && in_bf16 && norm_row2()) {
-      const dim3 g2((unsigned)((p.rows + 1) / 2));
-      if (p.bc_rows > 0) {
-        FLITE_REQUIRE(p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
-                      "rmsnorm(fp8 out): the deferred broadcast residual needs the rows in place");
-        hipLaunchKernelGGL((rmsnorm_mod_row2_kernel<true, false, true>), g2, dim3(256), 0, s, p);
-      } else {
-        hipLaunchKernelGGL((rmsnorm_mod_row2_kernel<true, false, false>), g2, dim3(256), 0, s, p);
-      }
-    } else if (p.D == 3072) {
+    if (p.D == 3072) {
       if (p.bc_rows > 0) {
         FLITE_REQUIRE(p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
                       "rmsnorm(fp8 out): the deferred broadcast residual needs the rows in place");
@@ -855,21 +712,6 @@ int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
         default: FLITE_REQUIRE(false, "rmsnorm(fp8 out): D must be 256, 512, 1024 or 3072");
       }
 #undef FLITE_NORM8_CASE
-    }
-    FLITE_HIP_CHECK(hipGetLastError());
-    return 0;
-  }
-  if (p.D == 3072 && p.rows < (1L << 31) && in_bf16 && norm_row2()) {  // bf16 residual: two rows per workgroup
-    const bool pf = p.pf[0] != nullptr || p.pf[1] != nullptr;
-    const dim3 g2((unsigned)((p.rows + 1) / 2));
-    if (p.bc_rows > 0) {
-      FLITE_REQUIRE(!pf && p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
-                    "rmsnorm: the deferred broadcast residual needs the rows in place, no read-ahead");
-      hipLaunchKernelGGL((rmsnorm_mod_row2_kernel<false, false, true>), g2, dim3(256), 0, s, p);
-    } else if (pf) {
-      hipLaunchKernelGGL((rmsnorm_mod_row2_kernel<false, true, false>), g2, dim3(256), 0, s, p);
-    } else {
-      hipLaunchKernelGGL((rmsnorm_mod_row2_kernel<false, false, false>), g2, dim3(256), 0, s, p);
     }
     FLITE_HIP_CHECK(hipGetLastError());
     return 0;

@@ -271,7 +271,7 @@ def test_attention_spike_rescale():
     assert rel(out, ref) < 1e-2
 
 
-# 3072: the one-workgroup-per-row kernel of the DiT width (bf16 rows: two per workgroup, rmsnorm_mod_row2_kernel);
+# 3072: the one-workgroup-per-row kernel of the DiT width (bf16 rows: the round-6 residual stream);
 # 602 rows: a partial last group of the 4-row kernel; 603 rows of 251: a lone last row and row pairs that straddle a
 # modulation segment
 @pytest.mark.parametrize("rows,T", [(602, 250), (603, 251)])
