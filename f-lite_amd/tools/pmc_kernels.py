@@ -28,6 +28,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--launches", type=int, default=6)
     ap.add_argument("--only", default=None, help="comma list of classes")
+    ap.add_argument("--residual", default="bf16", choices=["bf16", "fp32"],
+                    help="residual-stream storage of the proj / down epilogues and the norm input (round 6: bf16)")
     args = ap.parse_args()
     dev = "cuda"
     T, B, D, F, H, HD, LC = 4112, 2, 3072, 12288, 12, 256, 512
@@ -37,7 +39,10 @@ def main():
     def rnd(*shape, std=1.0):
         return (torch.randn(*shape, device=dev, generator=g) * std).bfloat16()
 
-    x = torch.randn(M, D, device=dev, generator=g) * 4  # fp32 residual stream
+    x = torch.randn(M, D, device=dev, generator=g) * 4  # the residual stream
+    if args.residual == "bf16":
+        x = x.bfloat16()
+    epi_resid = nat.EPI_RESID_BF16 if args.residual == "bf16" else nat.EPI_RESID_F32
     nbuf = rnd(M, D)
     w_qkv, b_qkv = rnd(3 * D, D, std=0.02), rnd(3 * D, std=0.02)
     w_proj = rnd(D, D, std=0.02)
@@ -74,7 +79,7 @@ def main():
             nat.attn_varlen(q3[:, 0], q3[:, 1], q3[:, 2], cu, cu, T, HD ** -0.5, out=obuf.view(M, H, HD),
                             max_score=16.5, workspace=aws, max_k=T)
         elif name == "proj":
-            nat.gemm(obuf, w_proj, out=x, epilogue=nat.EPI_RESID_F32, workspace=gws, **resid_kw)
+            nat.gemm(obuf, w_proj, out=x, epilogue=epi_resid, workspace=gws, **resid_kw)
         elif name == "rmsnorm_mod":
             nat.rmsnorm_modulate(x, wnorm, shift, scale, seg_rows=T, out=nbuf)
         elif name == "cross_q":
@@ -90,7 +95,7 @@ def main():
         elif name == "gateup":
             nat.gemm(nbuf, w_gate, out=hbuf, epilogue=nat.EPI_SWIGLU_BF16, w2=w_up, workspace=gws)
         elif name == "down":
-            nat.gemm(hbuf, w_down, out=x, epilogue=nat.EPI_RESID_F32, workspace=gws, **resid_kw)
+            nat.gemm(hbuf, w_down, out=x, epilogue=epi_resid, workspace=gws, **resid_kw)
 
     classes = args.only.split(",") if args.only else CLASSES
     torch.cuda.synchronize()
