@@ -126,6 +126,20 @@ static void engine_binds(int per_block, int bias) {
   EXPECT_ERR(eng.set_fp8_bf16_blocks(nullptr, 1), "bad block list");
   EXPECT_OK(eng.set_fp8_bf16_blocks(blks, 1));
   EXPECT_OK(eng.set_fp8_bf16_blocks(nullptr, 0));
+  std::vector<int> masks(c.depth, 63);
+  EXPECT_ERR(eng.set_fp8_block_classes(masks.data(), c.depth - 1), "one mask per block");
+  EXPECT_ERR(eng.set_fp8_block_classes(nullptr, c.depth), "one mask per block");
+  masks[0] = 64;
+  EXPECT_ERR(eng.set_fp8_block_classes(masks.data(), c.depth), "outside FLITE_FP8_ALL");
+  masks[0] = 0;
+  EXPECT_OK(eng.set_fp8_block_classes(masks.data(), c.depth));
+  EXPECT_OK(eng.set_fp8_block_classes(nullptr, 0));
+  EXPECT_OK(eng.set_residual_bf16(false));
+  if (eng.residual_bf16()) {
+    fprintf(stderr, "FAIL residual_bf16 after set_residual_bf16(false)\n");
+    ++failures;
+  }
+  EXPECT_OK(eng.set_residual_bf16(true));
   EXPECT_ERR(eng.forward(nullptr, p, false, 1, 2, 0, 0), "prepare first");
   EXPECT_ERR(eng.unpatchify_out(nullptr, nullptr, false), "prepare first");
   long a = 0, b = 0;
@@ -166,6 +180,12 @@ int main() {
   EXPECT_ERR(flite_apg_euler_dev(nullptr, f, f, f, 4, 6.f, 0.03f, 4, nullptr, 0.1f), "null");
   EXPECT_ERR(flite_apg_euler_dev(nullptr, f, f, f, 8, 6.f, 0.03f, 4, f, 0.1f), "element counts");
   EXPECT_ERR(flite_dit_set_fp8_bf16_blocks(nullptr, nullptr, 0), "null");
+  EXPECT_ERR(flite_dit_set_fp8_block_classes(nullptr, nullptr, 0), "null");
+  EXPECT_ERR(flite_dit_set_residual_bf16(nullptr, 1), "null");
+  if (flite_dit_residual_bf16(nullptr) != -1) {
+    fprintf(stderr, "FAIL flite_dit_residual_bf16(nullptr) != -1\n");
+    ++failures;
+  }
   // GEMM shape / stride / alignment validation happens before any kernel initialisation
   alignas(16) static char g[256];
   EXPECT_ERR(flite_gemm_bf16(nullptr, 0, 64, 64, g, 64, g, 64, nullptr, nullptr, 0, g, 64, nullptr, 0, 0), "empty");
