@@ -1,6 +1,7 @@
 """Reduce rocprofv3 passes over tools/pmc_kernels.py to per-kernel-class numbers (one JSON).
 
     python f-lite_amd/tools/pmc_reduce.py OUT.json trace=<dir> fetch=<dir> write=<dir> mfma=<dir> stall=<dir>
+        [residual=bf16|fp32]
 
 Each <dir> holds one rocprofv3 run (--output-format csv) of pmc_kernels.py; `trace` is a --kernel-trace run
 (durations at the un-profiled clock), the others one --pmc pass each:
@@ -36,7 +37,7 @@ WORK = {  # class -> (kind, algorithmic amount per launch: FLOP or bytes)
     "attn_cross": ("flop", 4.0 * B * H * T * LC * HD),
     "attn_cross_c": ("flop", 4.0 * 1 * H * T * LC * HD),  # uniform-context collapse: the cond sequence only
     "rope_qknorm": ("bytes", 2.0 * (M * 2 * D * 2)),       # q and k read + written, bf16
-    "rmsnorm_mod": ("bytes", M * D * 4.0 + M * D * 2.0),   # fp32 residual in, bf16 out
+    "rmsnorm_mod": ("bytes", M * D * 4.0 + M * D * 2.0),   # fp32 residual in, bf16 out (main: residual=bf16)
 }
 
 
@@ -86,6 +87,9 @@ def mean(v):
 def main():
     out_path = sys.argv[1]
     passes = dict(a.split("=", 1) for a in sys.argv[2:])
+    # residual=bf16 (round 6 default, pmc_kernels.py --residual bf16): the norm reads 2 B per element, not 4
+    if passes.pop("residual", "bf16") == "bf16":
+        WORK["rmsnorm_mod"] = ("bytes", M * D * 2.0 + M * D * 2.0)
     classes = json.loads(os.environ.get("PMC_CLASSES", "null"))
     if classes is None:  # the launch order of tools/pmc_kernels.py (marker k = classes[k])
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
