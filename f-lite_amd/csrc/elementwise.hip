@@ -231,149 +231,6 @@ __global__ __launch_bounds__(256) void rmsnorm_mod_row_kernel(NormModParams p) {
   }
 }
 
-// The bf16 residual stream (round 6) at D = 3072: one row per 128-thread workgroup (two waves), each thread 8
-// consecutive columns per 1024-column chunk, so every load and store moves 16 B per lane (the 256-thread one-row
-// kernel's bf16 form moves 8 B: 100 MB took 25.9 us at 0.49 of the HBM peak with 62 % of wave time waiting,
-// profiles/r06h), with as many workgroups as rows (the two-rows-per-workgroup forms lost, profiles/r06e, r06i).
-// Same per-element fp32 expression; the row sum is reduced over the two waves.
-// OUT8: a 32-column MX block is 4 consecutive lanes. BC / PF as in rmsnorm_mod_row_kernel.
-template <bool OUT8, bool PF, bool BC>
-__global__ __launch_bounds__(128) void rmsnorm_mod_h16_kernel(NormModParams p) {
-  constexpr int NQ = 3;
-  __shared__ float part[2];
-  const int t = threadIdx.x;
-  const int u = t;
-  const long m = blockIdx.x;
-  constexpr bool live = true;
-  const long mc = m;
-  const long seg = p.in_seg > 0 ? mc / p.in_seg : 0;
-  const long in_row = p.in_seg > 0 ? seg * p.in_stride + p.in_off + (mc % p.in_seg) : mc;
-  bf16_t* xr = (bf16_t*)p.x + in_row * p.ldx;
-  float v[NQ][8];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const u32x4 w = *(const u32x4*)(xr + q * 1024 + u * 8);
-    v[q][0] = __uint_as_float(w.x << 16);
-    v[q][1] = __uint_as_float(w.x & 0xffff0000u);
-    v[q][2] = __uint_as_float(w.y << 16);
-    v[q][3] = __uint_as_float(w.y & 0xffff0000u);
-    v[q][4] = __uint_as_float(w.z << 16);
-    v[q][5] = __uint_as_float(w.z & 0xffff0000u);
-    v[q][6] = __uint_as_float(w.w << 16);
-    v[q][7] = __uint_as_float(w.w & 0xffff0000u);
-  }
-  if constexpr (BC) {  // the bf16 deferred broadcast update (rmsnorm_mod_row_kernel), written back, then normalised
-    if (live && m < p.bc_rows) {
-      const long bs = m / p.bc_rows_per_seg;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int n = q * 1024 + u * 8;
-        const f32x4 c0 = *(const f32x4*)(p.bc_c + bs * 3072L + n), c1 = *(const f32x4*)(p.bc_c + bs * 3072L + n + 4);
-        const f32x4 g0 = *(const f32x4*)(p.bc_gate + bs * p.bc_gate_stride + n);
-        const f32x4 g1 = *(const f32x4*)(p.bc_gate + bs * p.bc_gate_stride + n + 4);
-        float nv[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          nv[j] = __builtin_fmaf(c0[j], g0[j], v[q][j]);
-          nv[4 + j] = __builtin_fmaf(c1[j], g1[j], v[q][4 + j]);
-        }
-        const u32x4 st = {pack2bf(nv[0], nv[1]), pack2bf(nv[2], nv[3]), pack2bf(nv[4], nv[5]), pack2bf(nv[6], nv[7])};
-        *(u32x4*)(xr + n) = st;
-        v[q][0] = __uint_as_float(st.x << 16);
-        v[q][1] = __uint_as_float(st.x & 0xffff0000u);
-        v[q][2] = __uint_as_float(st.y << 16);
-        v[q][3] = __uint_as_float(st.y & 0xffff0000u);
-        v[q][4] = __uint_as_float(st.z << 16);
-        v[q][5] = __uint_as_float(st.z & 0xffff0000u);
-        v[q][6] = __uint_as_float(st.w << 16);
-        v[q][7] = __uint_as_float(st.w & 0xffff0000u);
-      }
-    }
-  }
-  // weight, scale and shift before the reduction (their L2 round trip overlaps it), 8 columns each
-  const float* shift = p.shift ? p.shift + seg * p.mod_seg_stride : nullptr;
-  const float* scale = p.scale ? p.scale + seg * p.mod_seg_stride : nullptr;
-  float wgt[NQ][8];
-  f32x4 sc[NQ][2], sh[NQ][2];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int n = q * 1024 + u * 8;
-    if (p.w) {
-      const u32x4 ww = *(const u32x4*)(p.w + n);
-      wgt[q][0] = __uint_as_float(ww.x << 16);
-      wgt[q][1] = __uint_as_float(ww.x & 0xffff0000u);
-      wgt[q][2] = __uint_as_float(ww.y << 16);
-      wgt[q][3] = __uint_as_float(ww.y & 0xffff0000u);
-      wgt[q][4] = __uint_as_float(ww.z << 16);
-      wgt[q][5] = __uint_as_float(ww.z & 0xffff0000u);
-      wgt[q][6] = __uint_as_float(ww.w << 16);
-      wgt[q][7] = __uint_as_float(ww.w & 0xffff0000u);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) wgt[q][j] = 1.f;
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      sc[q][h] = scale ? *(const f32x4*)(scale + n + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
-      sh[q][h] = shift ? *(const f32x4*)(shift + n + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  float ss = 0.f;
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ss += v[q][j] * v[q][j];
-  ss = wave_sum(ss);
-  if ((t & 63) == 0) part[t >> 6] = ss;
-  __syncthreads();
-  const float rs = rsqrtf((part[0] + part[1]) / 3072.f + p.eps);
-  if (live) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int n = q * 1024 + u * 8;
-      float o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        o[j] = v[q][j] * rs * wgt[q][j] * (1.f + sc[q][j >> 2][j & 3]) + sh[q][j >> 2][j & 3];
-      if constexpr (OUT8) {
-        float amax = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(o[j]));
-        amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
-        amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
-        const int e = mx_exp(amax);
-        const float inv = mx_inv(e);
-        *(u32x2*)(p.y8 + m * p.ldy + n) = u32x2{pack4_fp8(o, inv), pack4_fp8(o + 4, inv)};
-        if ((n & 31) == 0) {
-          const int blk = n >> 5;
-          p.ysc[((long)(blk >> 2) * p.ysc_rows_pad + m) * 4 + (blk & 3)] = (uint8_t)(e + 127);
-        }
-      } else {
-        *(u32x4*)(p.y + m * p.ldy + n) =
-            u32x4{pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7])};
-      }
-    }
-  }
-  if constexpr (PF) {  // rmsnorm_mod_row_kernel's read-ahead, by workgroup
-    constexpr int NPF = 6;
-    unsigned pf_acc = 0;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      if (p.pf[r] == nullptr) continue;
-      const long pieces = p.pf_bytes[r] >> 11;  // 2 KiB pieces: 128 threads x 16 B
-      u32x4 pv[NPF];
-#pragma unroll
-      for (int k = 0; k < NPF; ++k) {
-        const long i = (long)blockIdx.x + (long)k * gridDim.x;
-        pv[k] = i < pieces ? ((const u32x4*)((const char*)p.pf[r] + (i << 11)))[t] : u32x4{0u, 0u, 0u, 0u};
-      }
-#pragma unroll
-      for (int k = 0; k < NPF; ++k) pf_acc ^= pv[k].x ^ pv[k].w;
-    }
-    if (p.pf_bytes[0] < 0 && pf_acc == 0x9e3779b9u) part[0] = 0.f;
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // RoPE (2-D, rotate-half pairs (j, j+128), rotation by -theta) + per-head RMSNorm (no weight), in place
 // on bf16 heads of 256. Reference: apply_rotary_emb (model.py:403-414) then QKNorm (model.py:115-126,180,197).
@@ -814,19 +671,6 @@ int grid_for(long total, int per_block = 256) {
   return (int)g;
 }
 
-// bf16 rows at D = 3072 take rmsnorm_mod_h16_kernel (FLITE_NORM_ROW1=1: the one-row kernel, an A/B switch)
-bool norm_h16() {
-  static const bool on = getenv("FLITE_NORM_ROW1") == nullptr;
-  return on;
-}
-// its 16-B accesses need 16-B aligned rows of x and y (8 elements) and of the parameter rows
-bool aligned16(const NormModParams& p) {
-  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
-  return p.ldx % 8 == 0 && al(p.x) && (p.y8 ? p.ldy % 8 == 0 && al(p.y8) : p.ldy % 8 == 0 && al(p.y)) &&
-         (!p.w || al(p.w)) && (!p.scale || (al(p.scale) && p.mod_seg_stride % 4 == 0)) &&
-         (!p.shift || al(p.shift)) && (!p.bc_c || al(p.bc_c)) && (!p.bc_gate || (al(p.bc_gate) && p.bc_gate_stride % 4 == 0));
-}
-
 }  // namespace
 
 int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
@@ -837,16 +681,7 @@ int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
   if (p.y8 != nullptr) {  // MXFP8 output (fp8 DiT path): fp32 or bf16 residual rows
     FLITE_REQUIRE(p.ysc != nullptr && p.ysc_rows_pad >= mx_rows_pad(p.rows) && p.D % 128 == 0 && p.ldy % 16 == 0,
                   "rmsnorm(fp8 out): scales for the padded rows, D % 128, 16-B row stride");
-    if (p.D == 3072 && in_bf16 && norm_h16() && aligned16(p)) {
-      const dim3 g2((unsigned)p.rows);
-      if (p.bc_rows > 0) {
-        FLITE_REQUIRE(p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
-                      "rmsnorm(fp8 out): the deferred broadcast residual needs the rows in place");
-        hipLaunchKernelGGL((rmsnorm_mod_h16_kernel<true, false, true>), g2, dim3(128), 0, s, p);
-      } else {
-        hipLaunchKernelGGL((rmsnorm_mod_h16_kernel<true, false, false>), g2, dim3(128), 0, s, p);
-      }
-    } else if (p.D == 3072) {
+    if (p.D == 3072) {
       if (p.bc_rows > 0) {
         FLITE_REQUIRE(p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
                       "rmsnorm(fp8 out): the deferred broadcast residual needs the rows in place");
@@ -877,21 +712,6 @@ int rmsnorm_mod(const NormModParams& p, bool in_bf16, hipStream_t s) {
         default: FLITE_REQUIRE(false, "rmsnorm(fp8 out): D must be 256, 512, 1024 or 3072");
       }
 #undef FLITE_NORM8_CASE
-    }
-    FLITE_HIP_CHECK(hipGetLastError());
-    return 0;
-  }
-  if (p.D == 3072 && p.rows < (1L << 31) && in_bf16 && norm_h16() && aligned16(p)) {  // bf16 rows: 16-B lanes
-    const bool pf = p.pf[0] != nullptr || p.pf[1] != nullptr;
-    const dim3 g2((unsigned)p.rows);
-    if (p.bc_rows > 0) {
-      FLITE_REQUIRE(!pf && p.in_seg == p.in_stride && p.in_off == 0 && p.bc_c && p.bc_gate && p.bc_rows_per_seg > 0,
-                    "rmsnorm: the deferred broadcast residual needs the rows in place, no read-ahead");
-      hipLaunchKernelGGL((rmsnorm_mod_h16_kernel<false, false, true>), g2, dim3(128), 0, s, p);
-    } else if (pf) {
-      hipLaunchKernelGGL((rmsnorm_mod_h16_kernel<false, true, false>), g2, dim3(128), 0, s, p);
-    } else {
-      hipLaunchKernelGGL((rmsnorm_mod_h16_kernel<false, false, false>), g2, dim3(128), 0, s, p);
     }
     FLITE_HIP_CHECK(hipGetLastError());
     return 0;
