@@ -52,6 +52,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="10b,7b")
     ap.add_argument("--policies", default=DEFAULT, help="'|'-separated policies ('bf16' = the bf16 path)")
+    ap.add_argument("--cfg", type=float, default=1.0, help="guidance (golden_full4 holds 1 and 6)")
     args = ap.parse_args()
     gdir = ROOT / "tests" / "golden"
     gd = load_file(str(gdir / "golden_full4.safetensors"))
@@ -64,7 +65,7 @@ def main():
         nat.init_param_(ctx, meta["inputs"]["ctx"][0], seed=0, std=1.0)
         lat = torch.empty(*meta["inputs"]["latents_1024"][1], device=dev, dtype=torch.bfloat16)
         nat.init_param_(lat, meta["inputs"]["latents_1024"][0], seed=0, std=1.0)
-        key = f"{name}.1024.s30.g1"
+        key = f"{name}.1024.s30.g{args.cfg:g}"
         for pol in args.policies.split("|"):
             if pol == "bf16":
                 m.enable_fp8(False)
@@ -73,10 +74,10 @@ def main():
                 masks = nat.fp8_block_masks(pol, cfg["depth"])
                 m.enable_fp8(True, block_classes=masks)
             out = FLitePipeline(m)(prompt_embeds=ctx, latents=lat.clone(), height=1024, width=1024,
-                                   num_inference_steps=30, guidance_scale=1.0,
+                                   num_inference_steps=30, guidance_scale=args.cfg,
                                    output_type="latent").images.float().cpu()
             p = psnr(out / 0.3611 + 0.1159, gd[f"{key}.f32.final"])
-            print(json.dumps({"model": name, "policy": pol or "all", "psnr_cfg1_vs_ref_fp32": round(p, 2),
+            print(json.dumps({"model": name, "policy": pol or "all", "cfg": args.cfg, "psnr_vs_ref_fp32": round(p, 2),
                               "fp8_flop_share": round(fp8_share(masks, cfg), 4),
                               "ref_bf16_vs_ref_fp32": round(meta.get(f"{key}.bf16_vs_f32_psnr", float("nan")), 2)}),
                   flush=True)
