@@ -71,7 +71,7 @@ def main():
                 m.enable_fp8(False)
                 masks = [0] * cfg["depth"]
             else:
-                masks = nat.fp8_block_masks(pol, cfg["depth"])
+                masks = nat.fp8_block_masks("" if pol == "all" else pol, cfg["depth"])
                 m.enable_fp8(True, block_classes=masks)
             out = FLitePipeline(m)(prompt_embeds=ctx, latents=lat.clone(), height=1024, width=1024,
                                    num_inference_steps=30, guidance_scale=args.cfg,
