@@ -393,9 +393,11 @@ struct GemmCta {
   // the fp32 residual: the loads of two accumulator rows (8 x + 8 gate, 16 B per lane) are issued together at
   // clamped, always-valid addresses and only the stores are masked, so the tile pays 4 memory round trips
   // instead of one per 16-B group (a bounds branch around each load makes hipcc wait vmcnt(0) per group).
-  // X16 (EPI_RESID_BF16): the residual stream is bf16, 8 B per 4 columns each way; the same fp32 expression, one
-  // rounding at the store.
-  template <bool GATED, bool TWO_SEG, bool X16 = false>
+  // X16 (EPI_RESID_BF16): the residual stream is bf16; the same fp32 expression, one rounding at the store.
+  // WIDE (X16 with N % 8 == 0 and 16-B aligned rows): the x loads and stores move 16 B per lane in common.h's deal8
+  // layout (8 consecutive columns of a 32-column pair of 16-column groups), one v_permlane16_swap per dword turning
+  // them into the accumulator layout and back (the swap is its own inverse); without it 8 B per 4 columns.
+  template <bool GATED, bool TWO_SEG, bool X16 = false, bool WIDE = false>
   __device__ __forceinline__ void resid_epilogue(const f32x4 (&acc)[8][4], int m_base, int n_base) {
     float bias[4][4];
     int nc[4];
@@ -437,9 +439,24 @@ struct GemmCta {
         orow[i] = (char*)p.out + (long)mc * p.ldo * XB;
         const int seg = GATED ? mc / p.rows_per_seg : 0;
         const float* grow = GATED ? p.gate + (long)seg * p.gate_seg_stride : nullptr;
+        if constexpr (WIDE) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int pc = n_base - lk * 4 + 32 * q + deal8_col();  // this lane's 8-column piece of the pair
+            const u32x4 w = *(const u32x4*)(orow[i] + (pc < p.N ? pc : 0) * XB);
+            const auto t = __builtin_amdgcn_permlane16_swap(w.x, w.z, false, false);  // deal8's inverse
+            const auto u = __builtin_amdgcn_permlane16_swap(w.y, w.w, false, false);
+            const u32x2 a = {t[0], u[0]}, b = {t[1], u[1]};  // groups 2q and 2q + 1 in the accumulator layout
+            xv[i][2 * q] = f32x4{__uint_as_float(a.x << 16), __uint_as_float(a.x & 0xffff0000u),
+                                 __uint_as_float(a.y << 16), __uint_as_float(a.y & 0xffff0000u)};
+            xv[i][2 * q + 1] = f32x4{__uint_as_float(b.x << 16), __uint_as_float(b.x & 0xffff0000u),
+                                     __uint_as_float(b.y << 16), __uint_as_float(b.y & 0xffff0000u)};
+          }
+        }
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
-          if constexpr (X16) {
+          if constexpr (WIDE) {
+          } else if constexpr (X16) {
             const u32x2 w = *(const u32x2*)(orow[i] + nc[ni] * XB);
             xv[i][ni] = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
                               __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
@@ -453,7 +470,8 @@ struct GemmCta {
         }
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i) {
+        u32x2 pk[4];
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           f32x4 x = xv[i][ni];
@@ -465,12 +483,23 @@ struct GemmCta {
             else
               x[r] += v;
           }
-          if constexpr (X16) {
+          if constexpr (WIDE) {
+            pk[ni] = u32x2{pack2bf(x[0], x[1]), pack2bf(x[2], x[3])};
+          } else if constexpr (X16) {
             if (mok[i] && nok[ni]) *(u32x2*)(orow[i] + nc[ni] * XB) = u32x2{pack2bf(x[0], x[1]), pack2bf(x[2], x[3])};
           } else {
             if (mok[i] && nok[ni]) *(f32x4*)(orow[i] + nc[ni] * XB) = x;
           }
         }
+        if constexpr (WIDE) {
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const u32x4 w = deal8(pk[2 * q], pk[2 * q + 1]);  // every lane takes part; only the store is masked
+            const int pc = n_base - lk * 4 + 32 * q + deal8_col();
+            if (mok[i] && pc < p.N) *(u32x4*)(orow[i] + pc * XB) = w;
+          }
+        }
+      }
     }
   }
 
@@ -602,14 +631,31 @@ struct GemmCta {
         }
       }
       return;
-    } else if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_RESID_BF16) {
-      constexpr bool X16 = EPI == EPI_RESID_BF16;
+    } else if constexpr (EPI == EPI_RESID_F32) {
       if (p.gate == nullptr)
-        resid_epilogue<false, false, X16>(acc, m_base, n_base);
+        resid_epilogue<false, false>(acc, m_base, n_base);
       else if (p.rows_per_seg >= MI * 16)
-        resid_epilogue<true, true, X16>(acc, m_base, n_base);
+        resid_epilogue<true, true>(acc, m_base, n_base);
       else
-        resid_epilogue<true, false, X16>(acc, m_base, n_base);
+        resid_epilogue<true, false>(acc, m_base, n_base);
+      return;
+    } else if constexpr (EPI == EPI_RESID_BF16) {
+      // 16-B lanes when every 8-column piece is inside or outside [0, N) and rows are 16-B aligned
+      if ((p.N & 7) == 0 && wide_ok() && !p.resid_narrow) {
+        if (p.gate == nullptr)
+          resid_epilogue<false, false, true, true>(acc, m_base, n_base);
+        else if (p.rows_per_seg >= MI * 16)
+          resid_epilogue<true, true, true, true>(acc, m_base, n_base);
+        else
+          resid_epilogue<true, false, true, true>(acc, m_base, n_base);
+      } else {
+        if (p.gate == nullptr)
+          resid_epilogue<false, false, true>(acc, m_base, n_base);
+        else if (p.rows_per_seg >= MI * 16)
+          resid_epilogue<true, true, true>(acc, m_base, n_base);
+        else
+          resid_epilogue<true, false, true>(acc, m_base, n_base);
+      }
       return;
     } else {
       float bias[4][4];
@@ -764,6 +810,10 @@ int launch(GemmParams p, hipStream_t s) {
   const int num_n = (p.N + BN - 1) / BN;
   const int T = (p.M + BM - 1) / BM * num_n;
   p.sk_tiles = choose_sk_tiles(p, T, &p.sk_wgs);
+  if constexpr (EPI == EPI_RESID_BF16) {
+    static const bool narrow = getenv("FLITE_GEMM_RESID_NARROW") != nullptr;  // A/B switch for measurements
+    p.resid_narrow = narrow;
+  }
   if (p.conv_in != nullptr) {
     if constexpr (EPI == EPI_STORE_BF16 || EPI == EPI_STORE_F32)  // gemm_bf16 admits only these with CONV
       hipLaunchKernelGGL((gemm_bf16_kernel<EPI, true, 8>), dim3(T), dim3(NT), LDS_ALLOC, s, p);

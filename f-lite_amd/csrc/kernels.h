@@ -52,6 +52,7 @@ struct GemmParams {
   // workgroups after their mainloops so that it comes from the Infinity Cache instead of HBM
   const void* pf = nullptr;
   long pf_bytes = 0;
+  int resid_narrow = 0;  // set by the launcher: EPI_RESID_BF16 with 8-B lanes (FLITE_GEMM_RESID_NARROW, A/B switch)
 };
 
 // bytes of the stream-K workspace (partials + flags) for the current device
