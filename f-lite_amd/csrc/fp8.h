@@ -65,6 +65,7 @@ struct GemmFp8Params {
   int* sk_flags = nullptr;
   int sk_tiles = 0;  // set by the launcher
   int sk_wgs = 0;    // set by the launcher
+  int resid_narrow = 0;  // set by the launcher: EPI8_RESID_BF16 with 8-B lanes (FLITE_GEMM_RESID_NARROW, A/B switch)
 };
 
 int gemm_fp8(const GemmFp8Params& p, int epi, hipStream_t s);

@@ -450,6 +450,58 @@ struct Fp8Cta {
 #pragma unroll
         for (int r = 0; r < 4; ++r) bias[ni][r] = (p.bias != nullptr && nok[ni]) ? bf2f(p.bias[nc[ni] + r]) : 0.f;
       }
+      if constexpr (X16) {
+        // 16-B lanes in the deal8 layout (gemm.hip resid_epilogue WIDE): same values, half the x instructions;
+        // two rows' loads issued before their stores, as below
+        if ((p.N & 7) == 0 && wide_ok() && !p.resid_narrow) {
+#pragma unroll
+          for (int mb = 0; mb < 8; mb += 2) {
+            unsigned xw[2][2][4];  // [row][q][dword], accumulator layout after the inverse deal
+            f32x4 gv[2][4];
+            char* orow[2];
+            bool mok[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              const int m = m_base + (mb + i) * 16;
+              mok[i] = mb + i < MI && m < p.M;
+              const int mc = mok[i] ? m : p.M - 1;
+              orow[i] = (char*)p.out + (long)mc * p.ldo * XB;
+              const float* grow = p.gate + (long)(mc / p.rows_per_seg) * p.gate_seg_stride;
+#pragma unroll
+              for (int ni = 0; ni < 4; ++ni)
+                gv[i][ni] = p.gate ? *(const f32x4*)(grow + nc[ni]) : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+              for (int q = 0; q < 2; ++q) {
+                const int pc = n_base - lk * 4 + 32 * q + deal8_col(lk);
+                const u32x4 w = *(const u32x4*)(orow[i] + (pc < p.N ? pc : 0) * XB);
+                const auto t = __builtin_amdgcn_permlane16_swap(w.x, w.z, false, false);  // deal8's inverse
+                const auto u = __builtin_amdgcn_permlane16_swap(w.y, w.w, false, false);
+                xw[i][q][0] = t[0], xw[i][q][1] = u[0], xw[i][q][2] = t[1], xw[i][q][3] = u[1];
+              }
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int q = 0; q < 2; ++q) {
+                u32x2 pk[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                  const int ni = 2 * q + h;
+                  const unsigned lo = xw[i][q][2 * h], hi = xw[i][q][2 * h + 1];
+                  f32x4 x = {__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+                             __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) x[r] += (acc[mb + i][ni][r] + bias[ni][r]) * gv[i][ni][r];
+                  pk[h] = u32x2{pack2bf(x[0], x[1]), pack2bf(x[2], x[3])};
+                }
+                const u32x4 o = deal8(pk[0], pk[1]);  // every lane takes part; only the store is masked
+                const int pc = n_base - lk * 4 + 32 * q + deal8_col(lk);
+                if (mok[i] && pc < p.N) *(u32x4*)(orow[i] + pc * XB) = o;
+              }
+          }
+          return;
+        }
+      }
 #pragma unroll
       for (int mb = 0; mb < 8; mb += 2) {
         f32x4 xv[2][4], gv[2][4];
@@ -597,6 +649,10 @@ bool bm224(const GemmFp8Params& p) {
 
 template <int EPI>
 void launch8(GemmFp8Params p, hipStream_t s) {
+  if constexpr (EPI == EPI8_RESID_BF16) {
+    static const bool narrow = getenv("FLITE_GEMM_RESID_NARROW") != nullptr;  // A/B switch for measurements
+    p.resid_narrow = narrow;
+  }
   const int num_n = (p.N + BN - 1) / BN;
   const int T = (p.M + 255) / 256 * num_n;
   p.sk_tiles = (p.sk_ws != nullptr && p.sk_flags != nullptr && g_sk_ok)
