@@ -421,6 +421,7 @@ struct Fp8Cta {
       const int oc0 = (n0 >> 1) + wave_n * 32;
       if (oc0 >= F) return;
       bf16_t* ob = (bf16_t*)p.out;
+      const bool wide = (F & 7) == 0 && wide_ok();  // an 8-column piece is inside or outside [0, F)
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
         const int m = m_base + mi * 16;
@@ -429,10 +430,15 @@ struct Fp8Cta {
         for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
           for (int r = 0; r < 4; ++r) h[4 * pr + r] = silu_f(acc[mi][2 * pr][r]) * acc[mi][2 * pr + 1][r];
-        if (m < p.M) {
+        const u32x2 lo = {pack2bf(h[0], h[1]), pack2bf(h[2], h[3])}, hi = {pack2bf(h[4], h[5]), pack2bf(h[6], h[7])};
+        if (wide) {  // common.h deal8: one 16-B piece per row instead of two 8-B pieces
+          const u32x4 w = deal8(lo, hi);
+          const int oc = oc0 + deal8_col(lk);
+          if (m < p.M && oc < F) *(u32x4*)(ob + (long)m * p.ldo + oc) = w;
+        } else if (m < p.M) {
           bf16_t* orow = ob + (long)m * p.ldo + oc0 + lk * 4;
-          *(u32x2*)(orow) = u32x2{pack2bf(h[0], h[1]), pack2bf(h[2], h[3])};
-          *(u32x2*)(orow + 16) = u32x2{pack2bf(h[4], h[5]), pack2bf(h[6], h[7])};
+          *(u32x2*)(orow) = lo;
+          *(u32x2*)(orow + 16) = hi;
         }
       }
       return;

@@ -123,6 +123,7 @@ EPI8_STORE_BF16 = 0
 EPI8_RESID_F32 = 2
 EPI8_RESID_BF16 = 7
 EPI8_SWIGLU_FP8 = 4
+EPI8_SWIGLU_BF16 = 6
 
 PROBE_GEMM_GATEUP = 0
 PROBE_ATTN_SELF = 1
@@ -484,7 +485,10 @@ def gemm_fp8(a8, a_sc, w8, w_sc, bias=None, *, out=None, epilogue=EPI8_STORE_BF1
     lib = load()
     M, K = a8.shape
     N = w8.shape[0]
-    if epilogue == EPI8_SWIGLU_FP8:
+    if epilogue == EPI8_SWIGLU_BF16:
+        if out is None:
+            out = torch.empty(M, N // 2, device=a8.device, dtype=torch.bfloat16)
+    elif epilogue == EPI8_SWIGLU_FP8:
         if out is None:
             out = torch.empty(M, N // 2, device=a8.device, dtype=torch.uint8)
         if out_sc is None:

@@ -136,6 +136,8 @@ int flite_rope_qknorm(void* stream, void* x, long ldx, long rows, int heads, int
 #define FLITE_EPI8_RESID_BF16 7  /* out_bf16[m][n]  = bf16(out + gate * (A.W^T + bias)), fp32 math     */
 #define FLITE_EPI8_SWIGLU_FP8 4  /* out_fp8[m][f]   = MX(silu(A.Wg^T) * (A.Wu^T)), W = gate|up interleaved in
                                     16-row sub-tiles (flite_quant_fp8_gateup), N = 2F; scales to out_scales */
+#define FLITE_EPI8_SWIGLU_BF16 6 /* out_bf16[m][f]  = silu(A.Wg^T) * (A.Wu^T), same W layout (an fp8 gate/up
+                                    feeding a bf16 down projection)                                  */
 
 /* bf16 rows [rows, K] (row stride ld_src elements) -> fp8 [rows, K] (row stride ld_dst bytes) + scales. */
 int flite_quant_fp8_rows(void* stream, const void* src, long ld_src, long rows, int K, void* dst, long ld_dst,

@@ -158,6 +158,16 @@ def test_gemm_fp8_swiglu():
     mism = (got != want).float().mean().item()
     print(f"fp8 SwiGLU GEMM: {p:.1f} dB vs fake-quant fp64; {mism * 100:.3f} % elements differ")
     assert p > 45 and mism < 0.02
+    # the bf16-output epilogue (an MXFP8 gate/up feeding a bf16 down): the same fp32 h rounded once, 16-B stores
+    hb = nat.gemm_fp8(a8, asc, gu8, gusc, epilogue=nat.EPI8_SWIGLU_BF16)
+    assert hb.dtype == torch.bfloat16 and hb.shape == (M, F)
+    assert ((hb.cpu().double() - h.double()).norm() / h.double().norm()).item() < 4e-3
+    assert (hb.cpu() != h.bfloat16()).float().mean().item() < 0.05
+    # a strided output (row stride F + 8: 16-B aligned rows) and one that is not 16-B aligned (8-B stores)
+    for pad in (8, 4):
+        buf = torch.zeros(M, F + pad, device=DEV, dtype=torch.bfloat16)
+        nat.gemm_fp8(a8, asc, gu8, gusc, epilogue=nat.EPI8_SWIGLU_BF16, out=buf[:, :F])
+        assert torch.equal(buf[:, :F], hb) and not buf[:, F:].any()
 
 
 @pytest.mark.parametrize("preset", ["tiny", "tiny_v2"])

@@ -62,6 +62,12 @@ def test_gemm_gated_residual_bf16(M, N, K, T):
     assert rel(x, ref) < 4e-3
     # most elements round to the same bf16 value (the only difference is the fp32 accumulation order)
     assert (x != ref).float().mean().item() < 0.05
+    # rows that are not 16-B aligned take the 8-B-lane epilogue: the same values bit for bit
+    buf = torch.zeros(M, N + 4, device=DEV, dtype=torch.bfloat16)
+    buf[:, :N] = x0
+    nat.gemm(a, w, b, out=buf[:, :N], epilogue=nat.EPI_RESID_BF16, gate=gate, gate_seg_stride=N, rows_per_seg=T,
+             workspace=nat.gemm_workspace(DEV) if K >= 4096 else None)
+    assert torch.equal(buf[:, :N], x) and not buf[:, N:].any()
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 256, 512), (8224, 3072, 3072), (8224, 3072, 12288)])
@@ -81,6 +87,12 @@ def test_gemm_fp8_gated_residual_bf16(M, N, K):
                  rows_per_seg=M, workspace=nat.gemm_workspace(DEV))
     # the same fp32 value (same kernel, same accumulation), rounded once at the store
     assert torch.equal(x, x32.bfloat16())
+    # rows that are not 16-B aligned take the 8-B-lane epilogue: the same values bit for bit
+    buf = torch.zeros(M, N + 4, device=DEV, dtype=torch.bfloat16)
+    buf[:, :N] = x0
+    nat.gemm_fp8(a8, asc, w8, wsc, out=buf[:, :N], epilogue=nat.EPI8_RESID_BF16, gate=gate, gate_seg_stride=0,
+                 rows_per_seg=M, workspace=nat.gemm_workspace(DEV))
+    assert torch.equal(buf[:, :N], x) and not buf[:, N:].any()
 
 
 @pytest.fixture(scope="module")
