@@ -784,6 +784,13 @@ int choose_sk_tiles(const GemmParams& p, int T, int* gs) {
   }
   static const bool no_sk = getenv("FLITE_GEMM_NO_SK") != nullptr;  // A/B switch for measurements
   if (no_sk) return 0;
+  // A/B switch for measurements: every short launch with a partial last round cut in FLITE_GEMM_SK_FAN ranges per
+  // leftover tile, whatever the model below predicts
+  static const int fan = getenv("FLITE_GEMM_SK_FAN") ? atoi(getenv("FLITE_GEMM_SK_FAN")) : 0;
+  if (fan >= 2 && G > 0 && rem > 0 && T / G < 8 && rem * (p.K / BK) >= 2 * std::min(G, fan * rem)) {
+    *gs = std::min(G, fan * rem);
+    return rem;
+  }
   return sk::choose_sk_tiles(T, p.K / BK, G, gs);
 }
 
